@@ -1,0 +1,240 @@
+"""ctypes binding of libanr_hip.so (the C ABI declared in include/anr.h).
+
+This is the only place Python touches the native library. Every kernel call goes
+through :func:`call`, which raises :class:`ANRError` with the library's message on a
+non-zero status. There is no fallback: if the library is missing or a tensor is not on
+a GPU, the call fails loudly.
+
+torch is imported first so that its HIP runtime (libamdhip64.so.7) is already loaded;
+libanr_hip.so then binds to that same runtime and can use torch's streams and memory.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (
+    POINTER,
+    Structure,
+    c_double,
+    c_float,
+    c_int32,
+    c_int64,
+    c_uint32,
+    c_void_p,
+)
+
+import torch  # noqa: F401  (must precede loading the HIP library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ANR_HIP_LIB", os.path.join(_HERE, "_native", "libanr_hip.so"))
+
+F32, F16 = 0, 1
+MAX_LEVELS = 32
+
+LOSS_CODES = {
+    "dark": 0,
+    "hdr": 1,
+    "l1": 2,
+    "l1_plus_hdr": 3,
+    "mse": 4,
+    "mse_plus_hdr": 5,
+}
+
+
+class ANRError(RuntimeError):
+    """A libanr_hip.so entry point returned an error status."""
+
+
+class PrepParams(Structure):
+    _fields_ = [
+        ("mode", c_int32),
+        ("shift_lon", c_int32),
+        ("ngp_remap", c_int32),
+        ("_pad", c_int32),
+        ("scale", c_double),
+        ("offset", c_double * 3),
+        ("lat_min", c_double),
+        ("lat_range", c_double),
+        ("lon_min", c_double),
+        ("lon_range", c_double),
+        ("ray_origin_height", c_double),
+        ("alt_compress", c_float),
+        ("_pad2", c_float),
+    ]
+
+
+class HashGridDesc(Structure):
+    _fields_ = [
+        ("n_dims", c_int32),
+        ("n_levels", c_int32),
+        ("n_features", c_int32),
+        ("base_resolution", c_int32),
+        ("per_level_scale", c_float),
+        ("log2_hashmap_size", c_int32),
+        ("n_params", c_int64),
+        ("offsets", c_uint32 * (MAX_LEVELS + 1)),
+        ("resolutions", c_uint32 * MAX_LEVELS),
+        ("scales", c_float * MAX_LEVELS),
+    ]
+
+
+class MlpDesc(Structure):
+    _fields_ = [
+        ("n_input", c_int32),
+        ("n_input_padded", c_int32),
+        ("n_output", c_int32),
+        ("n_output_padded", c_int32),
+        ("width", c_int32),
+        ("n_hidden_layers", c_int32),
+        ("activation", c_int32),
+        ("output_activation", c_int32),
+    ]
+
+
+# name -> (restype, argtypes). Mirrors include/anr.h one to one.
+_P = c_void_p
+_SIGNATURES = {
+    "anr_abi_version": (c_int32, []),
+    "anr_last_error": (ctypes.c_char_p, []),
+    "anr_sample_uniform_bins": (
+        c_int32,
+        [_P, _P, _P, _P, _P, c_int64, c_int32, _P, _P, POINTER(PrepParams), _P, _P],
+    ),
+    "anr_preprocess_points": (c_int32, [_P, c_int64, POINTER(PrepParams), _P, _P]),
+    "anr_hashgrid_init": (
+        c_int32,
+        [POINTER(HashGridDesc), c_int32, c_int32, c_int32, c_int32, c_float, c_int32],
+    ),
+    "anr_hashgrid_fwd": (
+        c_int32,
+        [POINTER(HashGridDesc), _P, c_int64, c_int64, _P, c_int32, _P, c_int32, c_int64, _P],
+    ),
+    "anr_hashgrid_bwd": (
+        c_int32,
+        [POINTER(HashGridDesc), _P, c_int64, c_int64, _P, c_int32, c_int64, _P, _P],
+    ),
+    "anr_sh_fwd": (c_int32, [c_int32, _P, c_int64, c_int64, _P, c_int32, c_int64, _P]),
+    "anr_sh_bwd": (
+        c_int32,
+        [c_int32, _P, c_int64, c_int64, _P, c_int32, c_int64, _P, c_int64, _P],
+    ),
+    "anr_identity": (
+        c_int32,
+        [_P, c_int32, c_int64, c_int64, c_int32, _P, c_int32, c_int64, _P],
+    ),
+    "anr_fill_cols": (c_int32, [_P, c_int32, c_int64, c_int64, c_int32, c_float, _P]),
+    "anr_mlp_n_params": (c_int64, [POINTER(MlpDesc)]),
+    "anr_mlp_fwd": (
+        c_int32,
+        [POINTER(MlpDesc), c_int32, _P, _P, c_int32, c_int64, c_int64, _P, c_int32, c_int64, _P],
+    ),
+    "anr_mlp_bwd": (
+        c_int32,
+        [
+            POINTER(MlpDesc), c_int32, _P, _P, c_int32, c_int64, c_int64, _P, c_int32,
+            c_int64, _P, c_int32, c_int64, _P, _P,
+        ],
+    ),
+    "anr_composite_fwd": (
+        c_int32,
+        [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, c_int32,
+         _P, _P, _P, _P, _P, _P],
+    ),
+    "anr_composite_bwd": (
+        c_int32,
+        [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, c_int32,
+         _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    ),
+    "anr_loss_workspace_bytes": (c_int64, [c_int64]),
+    "anr_loss_fwd_bwd": (
+        c_int32,
+        [c_int32, _P, c_int32, c_int32, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P],
+    ),
+    "anr_adam_step": (
+        c_int32,
+        [_P, _P, _P, _P, _P, c_int64, c_float, c_float, c_float, c_float, c_float,
+         c_int32, c_int64, c_int32, _P],
+    ),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libanr_hip.so (once) and declare every entry point's signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ANRError(
+            f"libanr_hip.so not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C csrc)"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def symbols() -> list[str]:
+    return list(_SIGNATURES)
+
+
+def call(name: str, *args) -> int:
+    """Call an entry point; raise ANRError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.anr_last_error().decode(errors="replace")
+        raise ANRError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def dtype_code(dtype: torch.dtype) -> int:
+    if dtype == torch.float32:
+        return F32
+    if dtype == torch.float16:
+        return F16
+    raise ANRError(f"unsupported dtype {dtype} (float32 / float16 only)")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    """Device pointer of a GPU tensor (None passes NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ANRError("libanr_hip kernels need GPU tensors (got a CPU tensor)")
+    return t.data_ptr()
+
+
+def stream(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def hashgrid_desc(n_dims: int, n_levels: int, n_features: int, base_resolution: int,
+                  per_level_scale: float, log2_hashmap_size: int) -> HashGridDesc:
+    d = HashGridDesc()
+    call("anr_hashgrid_init", ctypes.byref(d), n_dims, n_levels, n_features,
+         base_resolution, per_level_scale, log2_hashmap_size)
+    return d
+
+
+def mlp_desc(n_input: int, n_output: int, width: int, n_hidden_layers: int,
+             output_relu: bool) -> MlpDesc:
+    d = MlpDesc()
+    d.n_input = n_input
+    d.n_input_padded = (n_input + 15) // 16 * 16
+    d.n_output = n_output
+    d.n_output_padded = (n_output + 15) // 16 * 16
+    d.width = width
+    d.n_hidden_layers = n_hidden_layers
+    d.activation = 1
+    d.output_activation = 1 if output_relu else 0
+    n = load().anr_mlp_n_params(ctypes.byref(d))
+    if n < 0:
+        raise ANRError(load().anr_last_error().decode())
+    return d

@@ -1,0 +1,237 @@
+"""Synthetic HARP2-shaped scene (the benchmark and test dataset).
+
+No HARP2 L1B granule exists offline (the reference downloads them with earthaccess,
+src/atmonr/datasets/harp2.py:432-458), so this builds a scene with the same shape and
+the same ray pipeline as ``HARP2Dataset`` (harp2.py:26-429):
+
+* views in the HARP2 band layout, sorted into IRGB order (harp2.py:461-501): 90 views =
+  60 red + 10 each NIR/green/blue (S-full), or 2 per band (S-small);
+* view zeniths spread over [-45, 45] degrees along track;
+* a regular lat/lon pixel grid around (30N, 60W) at ~2.5 km spacing, surface altitude 0;
+* rays from ``get_rays`` -> ``filter_rays`` -> ``normalize_rays`` (wgs_84.py:223-339);
+* radiance from an analytic field: a band-dependent surface albedo pattern plus Gaussian
+  cloud blobs at 1-8 km whose image position moves with the view angle (parallax), so
+  the multi-angle views constrain a 3-D density.
+
+The object exposes the attributes and methods the pipelines and the trainer use from
+``HARP2Dataset``: ``config``, ``max_i``, ``lat``/``lon``/``alt``, ``scale``, ``offset``,
+``get_point_preprocessor``, ``__getbatch__``, ``__len__``, ``get_image_metrics``.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from .. import _lib
+from ..geospatial.wgs_84 import filter_rays, get_rays, normalize_rays
+from ..samplers import preprocess_points
+
+IRGB_WAVELENGTHS = (870.0, 670.0, 550.0, 440.0)  # NIR, red, green, blue
+
+
+@dataclass
+class PointPreprocessor:
+    """The "horizontal" preprocessor (harp2.py:357-388) as kernel parameters.
+
+    Calling it maps normalized scene points (..., 3) to [-1, 1]^3 (lat, lon, alt) on the
+    GPU (K2). ``params(ngp_remap=True, alt_compress=8)`` returns the struct the fused
+    sampler kernel takes.
+    """
+
+    scale: float
+    offset: tuple[float, float, float]
+    lat_min: float
+    lat_range: float
+    lon_min: float
+    lon_range: float
+    ray_origin_height: float
+    shift_lon: bool
+
+    def params(self, ngp_remap: bool = False, alt_compress: float = 1.0) -> _lib.PrepParams:
+        p = _lib.PrepParams()
+        p.mode = 1
+        p.shift_lon = int(self.shift_lon)
+        p.ngp_remap = int(ngp_remap)
+        p.scale = self.scale
+        for k in range(3):
+            p.offset[k] = self.offset[k]
+        p.lat_min, p.lat_range = self.lat_min, self.lat_range
+        p.lon_min, p.lon_range = self.lon_min, self.lon_range
+        p.ray_origin_height = self.ray_origin_height
+        p.alt_compress = alt_compress
+        return p
+
+    def __call__(self, coords_xyz: torch.Tensor) -> torch.Tensor:
+        return preprocess_points(coords_xyz, self.params())
+
+
+def make_preprocessor(lat: torch.Tensor, lon: torch.Tensor, scale: float,
+                      offset: torch.Tensor, ray_origin_height: float) -> PointPreprocessor:
+    """Ranges exactly as harp2.py:358-370 (f32 min/max over the non-NaN lat/lon)."""
+    la = lat[~lat.isnan()]
+    lo = lon[~lon.isnan()]
+    lat_min, lat_max = la.min(), la.max()
+    lon_min, lon_max = lo.min(), lo.max()
+    lat_range, lon_range = lat_max - lat_min, lon_max - lon_min
+    shift = bool(lon_max > 179 and lon_min < -179)
+    if shift:
+        lo = lo % 360 - 180
+        lon_min, lon_max = lo.min(), lo.max()
+        lon_range = lon_max - lon_min
+    off = offset.double().cpu().tolist()
+    return PointPreprocessor(float(scale), (off[0], off[1], off[2]), float(lat_min),
+                             float(lat_range), float(lon_min), float(lon_range),
+                             float(ray_origin_height), shift)
+
+
+def band_layout(n_views: int) -> list[int]:
+    """IRGB band index per view in IRGB-sorted order (NIR=0, red=1, green=2, blue=3)."""
+    if n_views == 90:
+        counts = [10, 60, 10, 10]
+    else:
+        if n_views % 4:
+            raise ValueError("n_views must be 90 or a multiple of 4")
+        counts = [n_views // 4] * 4
+    return [b for b, c in enumerate(counts) for _ in range(c)]
+
+
+class SyntheticHARP2Dataset:
+    """HARP2-shaped synthetic scene on a device (see module docstring)."""
+
+    def __init__(self, n_views: int = 90, img_size: int = 512, device="cuda",
+                 seed: int = 0, spacing_km: float = 2.5, center=(30.0, -60.0),
+                 max_abs_view_angle: float = 45.0, ray_origin_height: float = 20000.0,
+                 chunk: int = 1 << 22):
+        self.config = {
+            "type": "HARP2",
+            "max_abs_view_angle": max_abs_view_angle,
+            "ray_origin_height": ray_origin_height,
+            "bands_to_keep": [0, 1, 2, 3],
+            "rgb_mode": "nadir",
+        }
+        dev = torch.device(device)
+        self.device = dev
+        self.img_shp = (img_size, img_size)
+        g = torch.Generator().manual_seed(seed)
+        irgb = band_layout(n_views)
+        self.irgb_idx = torch.tensor(irgb, dtype=torch.int64)
+        self.view_idx = torch.arange(n_views)
+        # view angles: each band's views spread evenly over [-max, max]
+        angles = torch.zeros(n_views, dtype=torch.float64)
+        for b in range(4):
+            sel = [i for i, bb in enumerate(irgb) if bb == b]
+            k = len(sel)
+            vals = torch.linspace(-max_abs_view_angle, max_abs_view_angle, k) if k > 1 else torch.zeros(1)
+            angles[sel] = vals.double()
+        self.view_angles = angles
+        # pixel grid
+        dlat = spacing_km / 111.32
+        dlon = spacing_km / (111.32 * math.cos(math.radians(center[0])))
+        ii = torch.arange(img_size, dtype=torch.float64) - (img_size - 1) / 2
+        lat_px = center[0] - ii[:, None] * dlat + 0 * ii[None, :]   # north at the top
+        lon_px = center[1] + ii[None, :] * dlon + 0 * ii[:, None]
+        P, V = img_size * img_size, n_views
+        self.lat = lat_px.reshape(-1, 1).expand(P, V).float().to(dev).contiguous()
+        self.lon = lon_px.reshape(-1, 1).expand(P, V).float().to(dev).contiguous()
+        self.alt = torch.zeros(P, V, device=dev)
+        thetav = angles.abs().float()[None].expand(P, V).to(dev)
+        phiv = torch.where(angles >= 0, 0.0, 180.0).float()[None].expand(P, V).to(dev)
+
+        origins, dirs, lens = [], [], []
+        for s in range(0, P, max(1, chunk // V)):
+            e = min(P, s + max(1, chunk // V))
+            o, d, l = get_rays(self.lat[s:e], self.lon[s:e], self.alt[s:e], thetav[s:e],
+                               phiv[s:e], ray_origin_height)
+            origins.append(o)
+            dirs.append(d)
+            lens.append(l)
+        ray_origin = torch.cat(origins)
+        ray_dir = torch.cat(dirs)
+        ray_len = torch.cat(lens)
+        del origins, dirs, lens
+
+        self._blobs = self._make_blobs(g, center, img_size * spacing_km)
+        rad = self._radiance(self.lat.reshape(-1).double(), self.lon.reshape(-1).double(),
+                             angles.to(dev)[None].expand(P, V).reshape(-1),
+                             self.irgb_idx.to(dev)[None].expand(P, V).reshape(-1))
+        self.max_i = float(torch.nan_to_num(rad, nan=-1.0).max())
+        self.int_arr = rad.view(P, V).float()
+
+        self.ray_filter = filter_rays(ray_origin, ray_dir, rad)
+        self.ray_dir = ray_dir[self.ray_filter].contiguous()
+        self.ray_rad = rad[self.ray_filter].float().contiguous()
+        ray_len = ray_len[self.ray_filter]
+        self.ray_alt = self.alt.reshape(-1)[self.ray_filter]
+        self.ray_origin_norm, self.scale, self.offset = normalize_rays(
+            ray_origin[self.ray_filter], self.ray_dir, ray_len)
+        self.ray_len_norm = (ray_len / self.scale).contiguous()
+        self.ray_irgb_idx = self.irgb_idx.to(dev)[None].expand(P, V).reshape(-1)[self.ray_filter]
+        self.ray_irgb_idx = self.ray_irgb_idx.contiguous()
+        self.ray_idx = torch.arange(self.ray_origin_norm.shape[0], device=dev, dtype=torch.int64)
+        self._prep = make_preprocessor(self.lat, self.lon, self.scale, self.offset,
+                                       ray_origin_height)
+
+    # ------------------------------------------------------------------ radiance model
+    @staticmethod
+    def _make_blobs(g, center, extent_km):
+        blobs = []
+        for _ in range(5):
+            dy, dx = ((torch.rand(2, generator=g) - 0.5) * 0.6 * extent_km).tolist()
+            h = 1.0 + 7.0 * torch.rand(1, generator=g).item()          # km
+            r = extent_km * (0.04 + 0.08 * torch.rand(1, generator=g).item())
+            amp = 0.4 + 0.5 * torch.rand(1, generator=g).item()
+            blobs.append((dy, dx, h, r, amp))
+        return blobs
+
+    def _radiance(self, lat, lon, angle, band):
+        c_lat = float(lat.mean())
+        c_lon = float(lon.mean())
+        ky = (lat - c_lat) * 111.32
+        kx = (lon - c_lon) * 111.32 * math.cos(math.radians(c_lat))
+        albedo = torch.tensor([0.30, 0.18, 0.14, 0.12], dtype=torch.float64,
+                              device=lat.device)[band]
+        surf = albedo * (1.0 + 0.35 * torch.sin(kx / 37.0) * torch.cos(ky / 53.0))
+        tan = torch.tan(angle.double() * math.pi / 180)
+        cloud = torch.zeros_like(surf)
+        trans = torch.ones_like(surf)
+        for dy, dx, h, r, amp in self._blobs:
+            yy = ky - dy - h * tan                     # parallax along track
+            xx = kx - dx
+            blob = amp * torch.exp(-(yy * yy + xx * xx) / (r * r))
+            cloud = cloud + blob * (0.9 - 0.1 * band.double())
+            trans = trans * torch.exp(-2.0 * blob)
+        return (surf * trans + cloud) * 100.0
+
+    # ------------------------------------------------------------------ HARP2Dataset API
+    def get_point_preprocessor(self, point_preprocessor: str) -> PointPreprocessor:
+        if point_preprocessor != "horizontal":
+            raise NotImplementedError(point_preprocessor)
+        return self._prep
+
+    def __getbatch__(self, idx: torch.Tensor) -> dict[str, torch.Tensor]:
+        return {
+            "origin": self.ray_origin_norm[idx],
+            "dir": self.ray_dir[idx],
+            "alt": self.ray_alt[idx],
+            "rad": self.ray_rad[idx],
+            "len": self.ray_len_norm[idx],
+            "idx": self.ray_idx[idx],
+            "irgb_idx": self.ray_irgb_idx[idx],
+        }
+
+    __getitem__ = __getbatch__
+
+    def __len__(self) -> int:
+        return int(self.ray_origin_norm.shape[0])
+
+    def get_image_metrics(self, pred_img: torch.Tensor, target_img: torch.Tensor) -> dict:
+        """PSNR per view exactly as harp2.py:310-335 (torchmetrics' formula inlined)."""
+        pred = torch.clip(pred_img / self.max_i, 0, 1)
+        target = target_img / self.max_i
+        data_range = (target.max() - target.min()).item()
+        mse = ((pred - target) ** 2).mean(dim=(1, 2))
+        psnr = 10.0 * torch.log10(torch.tensor(data_range, dtype=mse.dtype) ** 2 / mse)
+        return {"PSNR": psnr.cpu().tolist(), "PSNR_mean": psnr[~torch.isnan(psnr)].mean().item()}

@@ -1,0 +1,210 @@
+"""InstantNGPPipeline — drop-in for src/atmonr/pipelines/instant_ngp.py on MI355X.
+
+Same constructor ``(config, dataset)``, module names, optimizer contract (AdamW with
+weight decay on the MLPs only, :107-127), ``forward`` result keys (:194-206),
+``extract`` (:208-247), ``compute_loss`` (:249-263) and nested ``state_dict``
+(:265-284). The six tinycudann modules (:60-85) are atmonr_amd.tcnn modules.
+
+Two execution paths, identical semantics:
+
+* ``fused=True`` (default, used by bench.py): K1+K2 sampler/preprocessor in one kernel,
+  the per-sample field as one autograd node (atmonr_amd.field.IngpFieldFn) with f32
+  gradients between kernels, the composite on K8 with z scaled in-kernel, the loss on K9.
+* ``fused=False``: the reference's op-by-op graph (sample_uniform_bins, the point
+  preprocessor, the (p+1)/2 remap, tcnn-style modules with f16 outputs) on the same
+  kernels — used to check that the fused path changes nothing but speed.
+"""
+
+from __future__ import annotations
+
+from itertools import chain
+from typing import Any, Mapping
+
+import torch
+import torch.nn.functional as F
+from torch.optim import Optimizer
+
+from .. import _lib
+from ..field import IngpFieldFn
+from ..graphics_utils import render_with_surface
+from ..losses import LOSSES, indexed_loss
+from ..optim import FusedAdam
+from ..samplers import preprocess_points, sample_and_preprocess, sample_uniform_bins
+from ..tcnn import Encoding, Network
+from .pipeline import Pipeline
+
+
+class InstantNGPPipeline(Pipeline):
+    module_names = ["pos_encoder", "pos_mlp", "dir_encoder", "dir_mlp", "surf_encoder",
+                    "surf_mlp"]
+
+    def __init__(self, config: dict, dataset: Any, dtype: torch.dtype = torch.float16,
+                 fused: bool = True, seed: int = 1337) -> None:
+        super().__init__(config, dataset)
+        self.num_density_outputs = 1
+        if self.config["multi_band_extinction"]:
+            self.num_density_outputs = self.config["num_bands"]
+        if self.config["include_height"]:
+            raise NotImplementedError("include_height is disabled in both reference configs")
+        if fused and self.num_density_outputs != 1:
+            fused = False
+        self.fused = fused
+        self.dtype = dtype
+        ingp = self.config["instant_ngp"]
+        nb = self.config["num_bands"]
+        fdt = torch.float32 if fused else None  # fused path keeps activations/grads in f32
+        self.pos_encoder = Encoding(3, ingp["encoding"], seed=seed, dtype=dtype)
+        self.pos_mlp = Network(self.pos_encoder.n_output_dims, 16, ingp["network"],
+                               seed=seed + 1, dtype=dtype)
+        self.dir_encoder = Encoding(3 + 16 - self.num_density_outputs, ingp["dir_encoding"],
+                                    seed=seed + 2, dtype=dtype)
+        self.dir_mlp = Network(self.dir_encoder.n_output_dims, nb, ingp["rgb_network"],
+                               seed=seed + 3, dtype=dtype)
+        self.surf_encoder = Encoding(2 + 3, ingp["surface_encoding"], seed=seed + 4,
+                                     dtype=dtype, output_dtype=fdt)
+        self.surf_mlp = Network(self.surf_encoder.n_output_dims, nb, ingp["surface_network"],
+                                seed=seed + 5, dtype=dtype, output_dtype=fdt)
+        d = self.dir_mlp.desc
+        self._dir_desc_relu = _lib.mlp_desc(d.n_input, d.n_output, d.width, d.n_hidden_layers,
+                                            True)
+        self.training = True
+        self.max_i = dataset.max_i
+        self.loss_name = self.config["loss"].lower()
+        self.loss_fn = LOSSES[self.loss_name]
+        self.alt_compress = float(self.config["alt_compress_factor"])
+        if self.point_preprocessor is not None:
+            self._prep_ngp = self.point_preprocessor.params(ngp_remap=True,
+                                                            alt_compress=self.alt_compress)
+
+    # ------------------------------------------------------------------ module plumbing
+    def modules(self):
+        return [getattr(self, n) for n in self.module_names]
+
+    def send_tensors_to(self, device: int) -> None:
+        self.device = device
+        for m in self.modules():
+            m.to(device)
+
+    def get_optimizer(self, config: dict, fused: bool = True) -> Optimizer:
+        """AdamW, weight decay on the MLPs only (instant_ngp.py:107-127)."""
+        no_decay = chain(self.pos_encoder.parameters(), self.dir_encoder.parameters(),
+                         self.surf_encoder.parameters())
+        decay = chain(self.pos_mlp.parameters(), self.dir_mlp.parameters(),
+                      self.surf_mlp.parameters())
+        groups = [
+            {"params": [p for p in no_decay if p.numel()], "weight_decay": 0},
+            {"params": list(decay), "weight_decay": config["weight_decay"]},
+        ]
+        kw = dict(config)
+        kw["betas"] = tuple(kw.get("betas", (0.9, 0.999)))
+        if fused:
+            return FusedAdam(groups, decoupled=True, **kw)
+        return torch.optim.AdamW(groups, **kw)
+
+    def parameters(self):
+        return chain(*(m.parameters() for m in self.modules()))
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, ray_batch: Mapping[str, torch.Tensor], u: torch.Tensor | None = None
+                ) -> dict[str, torch.Tensor]:
+        if self.fused:
+            return self._forward_fused(ray_batch, u)
+        return self._forward_reference(ray_batch, u)
+
+    def _surface(self, ray_batch):
+        # instant_ngp.py:143,150,173-174 (pts_surf in normalized Cartesian, then [0,1])
+        pts_surf = ray_batch["origin"] + ray_batch["dir"] * ray_batch["len"][:, None]
+        pts_surf = (pts_surf + 1) / 2
+        surf_in = torch.cat([pts_surf[:, :2], ray_batch["dir"]], dim=1)
+        return F.relu(self.surf_mlp(self.surf_encoder(surf_in)))
+
+    def _forward_fused(self, ray_batch, u=None):
+        B = ray_batch["origin"].shape[0]
+        N = self.config["num_samples_per_ray"]
+        _, z_vals, coords = sample_and_preprocess(ray_batch, N, self._prep_ngp, u=u)
+        sigma, color = IngpFieldFn.apply(coords.view(B * N, 3), ray_batch["dir"].float(), N,
+                                         self.pos_encoder.params, self.pos_mlp.params,
+                                         self.dir_mlp.params, self)
+        color = color.view(B, N, -1)
+        sigma = sigma.view(B, N, 1)
+        color_surf = self._surface(ray_batch)
+        color_map, _, weights, atmo, surf = render_with_surface(
+            z_vals, color, sigma, color_surf, z_scale=self.scale / 1000)
+        return {
+            "color_fine": color[:, :-1],
+            "color_surf": color_surf,
+            "color_map_surf": surf,
+            "color_map_atmo": atmo,
+            "sigma_fine": sigma[:, :-1],
+            "color_map_fine": color_map,
+            "weights_fine": weights,
+            "z_vals_fine": z_vals,
+        }
+
+    def _forward_reference(self, ray_batch, u=None):
+        # instant_ngp.py:137-206, op for op
+        B_ = ray_batch["origin"].shape[0]
+        N = self.config["num_samples_per_ray"]
+        pts, z_vals = sample_uniform_bins(ray_batch, N, u=u)
+        if self.point_preprocessor:
+            pts = self.point_preprocessor(pts)
+        pts = (pts + 1) / 2
+        dirs = ray_batch["dir"][:, None].repeat(1, N, 1)
+        pts[..., 2] = pts[..., 2] / self.config["alt_compress_factor"]
+        pos_enc = self.pos_encoder(pts.view(B_ * N, -1))
+        pos_out = self.pos_mlp(pos_enc)
+        dir_enc = self.dir_encoder(
+            torch.cat([dirs.view(B_ * N, 3), pos_out[:, self.num_density_outputs:]], dim=1))
+        color = self.dir_mlp(dir_enc).view(B_, N, self.config["num_bands"])
+        color_surf = self._surface(ray_batch)
+        sigma = pos_out[..., : self.num_density_outputs].view(B_, N, -1)
+        color = F.relu(color)
+        sigma = F.relu(sigma)
+        color_map, _, weights, atmo, surf = render_with_surface(
+            z_vals * (self.scale / 1000), color, sigma, color_surf)
+        return {
+            "color_fine": color[:, :-1],
+            "color_surf": color_surf,
+            "color_map_surf": surf,
+            "color_map_atmo": atmo,
+            "sigma_fine": sigma[:, :-1],
+            "color_map_fine": color_map,
+            "weights_fine": weights,
+            "z_vals_fine": z_vals,
+        }
+
+    def extract(self, pts: torch.Tensor) -> torch.Tensor:
+        """Extinction at normalized scene points (P,3) (instant_ngp.py:208-247)."""
+        if self.point_preprocessor:
+            pts = preprocess_points(pts, self._prep_ngp)
+        else:
+            pts = (pts + 1) / 2
+            pts[..., 2] = pts[..., 2] / self.alt_compress
+        with torch.no_grad():
+            pos_out = self.pos_mlp(self.pos_encoder(pts))
+        return torch.clip(pos_out[..., : self.num_density_outputs].view(
+            pts.shape[0], self.num_density_outputs), min=0)
+
+    def compute_loss(self, ray_batch: Mapping[str, torch.Tensor],
+                     results: dict[str, torch.Tensor]) -> torch.Tensor:
+        """loss_fn(take_along_dim(color_map, irgb_idx), rad, max_i) (instant_ngp.py:249-263)."""
+        return indexed_loss(self.loss_name, results["color_map_fine"], ray_batch["irgb_idx"],
+                            ray_batch["rad"], self.max_i)
+
+    # ------------------------------------------------------------------ state
+    def state_dict(self) -> Mapping[str, Mapping[str, Any]]:
+        return {n: getattr(self, n).state_dict() for n in self.module_names}
+
+    def load_state_dict(self, state_dict: dict) -> None:
+        for n in self.module_names:
+            getattr(self, n).load_state_dict(state_dict[n])
+
+    def train(self) -> None:
+        self.training = True
+        for m in self.modules():
+            m.train()
+
+    def eval(self) -> None:
+        self.training = False
+        for m in self.modules():
+            m.eval()

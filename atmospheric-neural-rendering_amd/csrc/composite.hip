@@ -1,0 +1,373 @@
+// K8: transmittance / alpha-composite integrator, forward and backward.
+//
+// Replaces render() and render_with_surface() at src/atmonr/graphics_utils.py:6-77
+// (called at src/atmonr/pipelines/instant_ngp.py:187-192 with z_vals*(scale/1000) and
+// at pipelines/nerf.py:156). Reference math per ray (graphics_utils.py:28-48, 75-76):
+//   mid   = [0, (z_i + z_{i+1})/2 ..., z_{N-1}]        delta_i = mid_{i+1} - mid_i
+//   alpha = 1 - exp(-sigma * delta)                    t_i = 1 - alpha_i + 1e-10
+//   T_i   = prod_{j<i} t_j (cumprod)                   w_i = alpha_i * T_i
+//   C_atmo = sum_i w_i * c_i      C_surf = prod_i (1 - alpha_i) * c_surf
+//   C = C_atmo + C_surf
+// One wavefront per ray; lane l owns the contiguous samples [l*spl, (l+1)*spl). The
+// cumprod is a lane-local product followed by a 64-lane shuffle exclusive scan; sums
+// and the full product are shuffle reductions. The backward (autograd of the above)
+// needs two suffix quantities, computed with reverse shuffle scans:
+//   dL/dalpha_i = T_i (q_i - U_i) - r * prod_{k!=i}(1 - alpha_k) + dL/dalpha_i(direct)
+//   U_i = sum_{j>i} q_j alpha_j prod_{i<k<j} t_k   (affine suffix scan; no division)
+// with q_i = dL/dw_i and r = dL/dC_surf-product, so it stays exact when alpha -> 1.
+// Arithmetic is f32 regardless of the storage dtype.
+#pragma clang fp contract(off)
+
+#include "anr_common.h"
+
+namespace anr {
+
+constexpr int kMaxCh = 8;
+
+template <typename T>
+__device__ __forceinline__ float ldv(const T* p, int64_t i) { return to_f32<T>(p[i]); }
+
+// Exclusive multiplicative scan across the wave (lane 0 gets 1).
+__device__ __forceinline__ float wave_excl_prod(float v, int lane) {
+  float incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const float o = shfl_up(incl, d);
+    if (lane >= d) incl *= o;
+  }
+  const float ex = shfl_up(incl, 1);
+  return lane == 0 ? 1.0f : ex;
+}
+// Exclusive multiplicative suffix scan (lane 63 gets 1).
+__device__ __forceinline__ float wave_excl_suffix_prod(float v, int lane) {
+  float incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const float o = shfl_down(incl, d);
+    if (lane + d < 64) incl *= o;
+  }
+  const float ex = shfl_down(incl, 1);
+  return lane == 63 ? 1.0f : ex;
+}
+__device__ __forceinline__ float wave_prod(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v *= shfl_xor(v, m);
+  return v;
+}
+// Reverse affine scan: lane holds map x -> A*x + B for its block; returns the value
+// entering the lane's block from the right, i.e. (composition of lanes > l)(0).
+__device__ __forceinline__ float wave_affine_suffix(float A, float B, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const float Ao = shfl_down(A, d);
+    const float Bo = shfl_down(B, d);
+    if (lane + d < 64) {
+      B = A * Bo + B;
+      A = A * Ao;
+    }
+  }
+  const float nxt = shfl_down(B, 1);
+  return lane == 63 ? 0.0f : nxt;
+}
+
+struct CompArgs {
+  const float* z;
+  float z_scale;
+  const void* color;
+  const void* sigma;
+  const void* color_surf;
+  int64_t B;
+  int N, C, S;
+  // forward outputs
+  void *color_map, *atmo, *surf, *weights, *alpha;
+  // backward inputs / outputs
+  const void *d_color_map, *d_atmo, *d_surf, *d_weights, *d_alpha;
+  void *d_color, *d_sigma, *d_color_surf;
+  float* d_z;
+};
+
+// delta_i for sample i of a ray (graphics_utils.py:30-34), z already in the ray's row.
+__device__ __forceinline__ float delta_at(const float* zr, float zs, int i, int N) {
+  const float zi = zr[i] * zs;
+  const float lo = i == 0 ? zr[0] * zs * 0.0f : (zr[i - 1] * zs + zi) / 2.0f;
+  const float hi = i == N - 1 ? zi : (zi + zr[i + 1] * zs) / 2.0f;
+  return hi - lo;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) composite_fwd_kernel(CompArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
+  if (b >= a.B) return;
+  const int N = a.N, C = a.C, S = a.S;
+  const int spl = (N + 63) / 64;
+  const int i0 = lane * spl;
+  const int i1 = min(i0 + spl, N);
+  const float* zr = a.z + b * N;
+  const T* sig = static_cast<const T*>(a.sigma) + b * N * S;
+  const T* col = static_cast<const T*>(a.color) + b * N * C;
+
+  // pass 1: lane products of t and (1 - alpha)
+  float pt[kMaxCh], pom[kMaxCh];
+#pragma unroll
+  for (int s = 0; s < kMaxCh; ++s) pt[s] = pom[s] = 1.0f;
+  for (int i = i0; i < i1; ++i) {
+    const float dl = delta_at(zr, a.z_scale, i, N);
+#pragma unroll
+    for (int s = 0; s < kMaxCh; ++s) {
+      if (s < S) {
+        const float al = 1.0f - expf(-ldv(sig, i * S + s) * dl);
+        pt[s] *= (1.0f - al) + 1e-10f;
+        pom[s] *= 1.0f - al;
+      }
+    }
+  }
+  float T_in[kMaxCh], Stot[kMaxCh];
+#pragma unroll
+  for (int s = 0; s < kMaxCh; ++s) {
+    if (s < S) {
+      T_in[s] = wave_excl_prod(pt[s], lane);
+      Stot[s] = wave_prod(pom[s]);
+    }
+  }
+  // pass 2: weights and the atmospheric sum
+  float cm[kMaxCh];
+#pragma unroll
+  for (int c = 0; c < kMaxCh; ++c) cm[c] = 0.0f;
+  for (int i = i0; i < i1; ++i) {
+    const float dl = delta_at(zr, a.z_scale, i, N);
+    float w[kMaxCh];
+#pragma unroll
+    for (int s = 0; s < kMaxCh; ++s) {
+      if (s < S) {
+        const float al = 1.0f - expf(-ldv(sig, i * S + s) * dl);
+        w[s] = al * T_in[s];
+        T_in[s] *= (1.0f - al) + 1e-10f;
+        const int64_t o = (b * N + i) * S + s;
+        if (a.weights) static_cast<T*>(a.weights)[o] = from_f32<T>(w[s]);
+        if (a.alpha) static_cast<T*>(a.alpha)[o] = from_f32<T>(al);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kMaxCh; ++c)
+      if (c < C) cm[c] += ldv(col, i * C + c) * w[S == 1 ? 0 : c];
+  }
+#pragma unroll
+  for (int c = 0; c < kMaxCh; ++c) {
+    if (c < C) {
+      const float atmo = wave_sum(cm[c]);
+      float surf = 0.0f;
+      if (a.color_surf)
+        surf = Stot[S == 1 ? 0 : c] * ldv(static_cast<const T*>(a.color_surf), b * C + c);
+      if (lane == 0) {
+        static_cast<T*>(a.color_map)[b * C + c] = from_f32<T>(atmo + surf);
+        if (a.atmo) static_cast<T*>(a.atmo)[b * C + c] = from_f32<T>(atmo);
+        if (a.surf) static_cast<T*>(a.surf)[b * C + c] = from_f32<T>(surf);
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) composite_bwd_kernel(CompArgs a) {
+  // Per wave LDS: lane-local prefix products Tloc, Ploc (N*S each) and dL/d(delta) (N).
+  extern __shared__ float lds[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x / 64;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * (blockDim.x / 64) + wv;
+  const bool active = b < a.B;
+  const int N = a.N, C = a.C, S = a.S;
+  float* Tloc = lds + static_cast<int64_t>(wv) * (2 * S + 1) * N;
+  float* Ploc = Tloc + N * S;
+  float* dD = Ploc + N * S;
+  const int spl = (N + 63) / 64;
+  const int i0 = lane * spl;
+  const int i1 = min(i0 + spl, N);
+  const int64_t bb = active ? b : 0;
+  const T* sig = static_cast<const T*>(a.sigma) + bb * N * S;
+  const T* col = static_cast<const T*>(a.color) + bb * N * C;
+  const float* zr = a.z + bb * N;
+
+  // per-ray upstream gradients: g_atmo = dC + dC_atmo, g_surf = dC + dC_surf
+  float ga[kMaxCh], gs[kMaxCh];
+#pragma unroll
+  for (int c = 0; c < kMaxCh; ++c) {
+    ga[c] = gs[c] = 0.0f;
+    if (c < C && active) {
+      const float dc = a.d_color_map ? ldv(static_cast<const T*>(a.d_color_map), bb * C + c) : 0.0f;
+      ga[c] = dc + (a.d_atmo ? ldv(static_cast<const T*>(a.d_atmo), bb * C + c) : 0.0f);
+      gs[c] = dc + (a.d_surf ? ldv(static_cast<const T*>(a.d_surf), bb * C + c) : 0.0f);
+    }
+  }
+
+  // pass 1 (forward over the lane's block): lane products of t and 1-alpha, local
+  // prefixes to LDS, and the block's reverse affine map of V_i = q_i*alpha_i + t_i*V_{i+1}
+  // accumulated left-to-right as (A, B) <- (A*t_i, B + A*q_i*alpha_i).
+  float pt[kMaxCh], pom[kMaxCh], A[kMaxCh], Bv[kMaxCh];
+#pragma unroll
+  for (int s = 0; s < kMaxCh; ++s) { pt[s] = pom[s] = A[s] = 1.0f; Bv[s] = 0.0f; }
+  if (active) {
+    for (int i = i0; i < i1; ++i) {
+      const float dl = delta_at(zr, a.z_scale, i, N);
+      float q[kMaxCh];
+#pragma unroll
+      for (int s = 0; s < kMaxCh; ++s) q[s] = 0.0f;
+#pragma unroll
+      for (int c = 0; c < kMaxCh; ++c)
+        if (c < C) q[S == 1 ? 0 : c] += ldv(col, i * C + c) * ga[c];
+#pragma unroll
+      for (int s = 0; s < kMaxCh; ++s)
+        if (s < S) {
+          if (a.d_weights) q[s] += ldv(static_cast<const T*>(a.d_weights), (bb * N + i) * S + s);
+          const float al = 1.0f - expf(-ldv(sig, i * S + s) * dl);
+          const float t = (1.0f - al) + 1e-10f;
+          Tloc[i * S + s] = pt[s];
+          Ploc[i * S + s] = pom[s];
+          pt[s] *= t;
+          pom[s] *= 1.0f - al;
+          Bv[s] = Bv[s] + A[s] * q[s] * al;
+          A[s] = A[s] * t;
+        }
+    }
+  }
+  float T_in[kMaxCh], P_in[kMaxCh], Q[kMaxCh], V[kMaxCh], Stot[kMaxCh], r[kMaxCh];
+#pragma unroll
+  for (int s = 0; s < kMaxCh; ++s) {
+    r[s] = 0.0f;
+    if (s < S) {
+      T_in[s] = wave_excl_prod(pt[s], lane);
+      P_in[s] = wave_excl_prod(pom[s], lane);
+      Q[s] = wave_excl_suffix_prod(pom[s], lane);
+      Stot[s] = wave_prod(pom[s]);
+      V[s] = wave_affine_suffix(A[s], Bv[s], lane);
+    }
+  }
+  if (a.color_surf && active) {
+#pragma unroll
+    for (int c = 0; c < kMaxCh; ++c)
+      if (c < C) r[S == 1 ? 0 : c] += ldv(static_cast<const T*>(a.color_surf), bb * C + c) * gs[c];
+  }
+
+  // pass 2 (reverse over the lane's block): per-sample gradients.
+  if (active) {
+    for (int i = i1 - 1; i >= i0; --i) {
+      const float dl = delta_at(zr, a.z_scale, i, N);
+      float q[kMaxCh];
+#pragma unroll
+      for (int s = 0; s < kMaxCh; ++s) q[s] = 0.0f;
+#pragma unroll
+      for (int c = 0; c < kMaxCh; ++c)
+        if (c < C) q[S == 1 ? 0 : c] += ldv(col, i * C + c) * ga[c];
+      float dd = 0.0f;  // dL/d(delta_i), summed over density channels
+#pragma unroll
+      for (int s = 0; s < kMaxCh; ++s)
+        if (s < S) {
+          const int64_t o = (bb * N + i) * S + s;
+          if (a.d_weights) q[s] += ldv(static_cast<const T*>(a.d_weights), o);
+          const float sg = ldv(sig, i * S + s);
+          const float e = expf(-sg * dl);
+          const float al = 1.0f - e;
+          const float t = (1.0f - al) + 1e-10f;
+          const float Ti = T_in[s] * Tloc[i * S + s];
+          const float Pi = P_in[s] * Ploc[i * S + s];
+          const float w = al * Ti;
+#pragma unroll
+          for (int c = 0; c < kMaxCh; ++c)
+            if (c < C && (S == 1 || c == s) && a.d_color)
+              static_cast<T*>(a.d_color)[(bb * N + i) * C + c] = from_f32<T>(w * ga[c]);
+          float dal = Ti * (q[s] - V[s]) - r[s] * Pi * Q[s];
+          if (a.d_alpha) dal += ldv(static_cast<const T*>(a.d_alpha), o);
+          // alpha = 1 - exp(-sigma*delta): d/dsigma = delta*e, d/ddelta = sigma*e
+          if (a.d_sigma) static_cast<T*>(a.d_sigma)[o] = from_f32<T>(dal * e * dl);
+          dd += dal * e * sg;
+          V[s] = q[s] * al + t * V[s];
+          Q[s] *= 1.0f - al;
+        }
+      if (a.d_z) dD[i] = dd;
+    }
+  }
+  if (a.d_color_surf && active && lane == 0) {
+#pragma unroll
+    for (int c = 0; c < kMaxCh; ++c)
+      if (c < C)
+        static_cast<T*>(a.d_color_surf)[bb * C + c] = from_f32<T>(Stot[S == 1 ? 0 : c] * gs[c]);
+  }
+  if (a.d_z) {
+    __syncthreads();
+    if (active) {
+      // delta_i = mid_{i+1} - mid_i, mid_j = (zs_{j-1} + zs_j)/2 for 1 <= j <= N-1,
+      // mid_0 = 0, mid_N = zs_{N-1}; zs = z * z_scale.
+      for (int j = i0; j < i1; ++j) {
+        float g = 0.0f;
+        if (j >= 1) g += 0.5f * (dD[j - 1] - dD[j]);
+        if (j + 1 <= N - 1) g += 0.5f * (dD[j] - dD[j + 1]);
+        if (j == N - 1) g += dD[N - 1];
+        a.d_z[bb * N + j] = g * a.z_scale;
+      }
+    }
+  }
+}
+
+}  // namespace anr
+
+extern "C" int anr_composite_fwd(const float* z, float z_scale, const void* color,
+                                 const void* sigma, const void* color_surf, int32_t io_dtype,
+                                 int64_t B, int32_t N, int32_t C, int32_t S, void* color_map,
+                                 void* color_map_atmo, void* color_map_surf, void* weights,
+                                 void* alpha, anr_stream_t stream) {
+  using namespace anr;
+  if (B == 0) return ANR_OK;
+  ANR_CHECK_ARG(z && color && sigma && color_map, "anr_composite_fwd: null argument");
+  ANR_CHECK_ARG(B >= 0 && N >= 1 && C >= 1 && C <= kMaxCh && (S == 1 || S == C),
+                "anr_composite_fwd: bad shape B=%lld N=%d C=%d S=%d", (long long)B, N, C, S);
+  ANR_CHECK_ARG(io_dtype == ANR_F16 || io_dtype == ANR_F32, "anr_composite_fwd: bad dtype");
+  if (B == 0) return ANR_OK;
+  CompArgs a{};
+  a.z = z; a.z_scale = z_scale; a.color = color; a.sigma = sigma; a.color_surf = color_surf;
+  a.B = B; a.N = N; a.C = C; a.S = S;
+  a.color_map = color_map; a.atmo = color_map_atmo; a.surf = color_map_surf;
+  a.weights = weights; a.alpha = alpha;
+  const dim3 grid(static_cast<unsigned>(ceil_div(B, 4))), block(256);
+  if (io_dtype == ANR_F16)
+    hipLaunchKernelGGL(composite_fwd_kernel<__half>, grid, block, 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(composite_fwd_kernel<float>, grid, block, 0, as_stream(stream), a);
+  ANR_CHECK_LAUNCH("anr_composite_fwd");
+  return ANR_OK;
+}
+
+extern "C" int anr_composite_bwd(const float* z, float z_scale, const void* color,
+                                 const void* sigma, const void* color_surf, int32_t io_dtype,
+                                 int64_t B, int32_t N, int32_t C, int32_t S,
+                                 const void* d_color_map, const void* d_atmo,
+                                 const void* d_surf, const void* d_weights,
+                                 const void* d_alpha, void* d_color, void* d_sigma,
+                                 void* d_color_surf, float* d_z, anr_stream_t stream) {
+  using namespace anr;
+  if (B == 0) return ANR_OK;
+  ANR_CHECK_ARG(z && color && sigma, "anr_composite_bwd: null argument");
+  ANR_CHECK_ARG(B >= 0 && N >= 1 && C >= 1 && C <= kMaxCh && (S == 1 || S == C),
+                "anr_composite_bwd: bad shape");
+  ANR_CHECK_ARG(io_dtype == ANR_F16 || io_dtype == ANR_F32, "anr_composite_bwd: bad dtype");
+  ANR_CHECK_ARG(d_color_surf == nullptr || color_surf != nullptr,
+                "anr_composite_bwd: d_color_surf without color_surf");
+  if (B == 0) return ANR_OK;
+  CompArgs a{};
+  a.z = z; a.z_scale = z_scale; a.color = color; a.sigma = sigma; a.color_surf = color_surf;
+  a.B = B; a.N = N; a.C = C; a.S = S;
+  a.d_color_map = d_color_map; a.d_atmo = d_atmo; a.d_surf = d_surf;
+  a.d_weights = d_weights; a.d_alpha = d_alpha;
+  a.d_color = d_color; a.d_sigma = d_sigma; a.d_color_surf = d_color_surf; a.d_z = d_z;
+  const size_t per_wave = static_cast<size_t>(2 * S + 1) * N * sizeof(float);
+  int waves = 4;
+  while (waves > 1 && waves * per_wave > 64 * 1024) --waves;
+  const size_t lds = waves * per_wave;
+  ANR_CHECK_ARG(lds <= 64 * 1024, "anr_composite_bwd: N*S too large (%d*%d)", N, S);
+  const dim3 grid(static_cast<unsigned>(ceil_div(B, waves))), block(64 * waves);
+  if (io_dtype == ANR_F16)
+    hipLaunchKernelGGL(composite_bwd_kernel<__half>, grid, block, lds, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(composite_bwd_kernel<float>, grid, block, lds, as_stream(stream), a);
+  ANR_CHECK_LAUNCH("anr_composite_bwd");
+  return ANR_OK;
+}

@@ -1,0 +1,420 @@
+// K3 / K4: multi-resolution hash-grid encoding, forward and backward.
+//
+// Replaces tinycudann.Encoding(n, {"otype": "HashGrid", ...}) at
+// src/atmonr/pipelines/instant_ngp.py:60-63 (3-D positions, called at :163/:236) and the
+// 2-D surface grid nested in the surface Composite (:78-80, called at :173).
+// Semantics (tiny-cuda-nn GridEncoding; the reference pins no version — see DESIGN.md):
+//   scale_l = 2^(l * log2(per_level_scale)) * base_resolution - 1     (f32)
+//   res_l   = ceil(scale_l) + 1
+//   pos     = fma(scale_l, x, 0.5); cell = floor(pos); w = pos - cell (linear)
+//   index   = dense stride index while stride <= T_l, else XOR prime hash; % T_l
+//   out[l*F + f] = sum over 2^D corners of prod(w or 1-w) * table[(off_l + index)*F + f]
+//
+// Work decomposition (MI355X-specific): one thread owns one LEVEL of a CHUNK of K
+// consecutive samples. Samples are ray-major, so consecutive samples of a ray usually
+// stay in the same cell of a level (always on the coarse levels, ~4 samples per cell on
+// the finest). The forward keeps the 2^D corner features of the current cell in
+// registers and re-gathers only when the cell changes; the backward accumulates the
+// corner gradients of the current cell in registers and issues the f32 atomics only
+// when the cell changes. Lanes of a wavefront are the levels of one chunk (16 levels ->
+// 4 chunks per wave): the per-sample coordinate load is a broadcast and the per-sample
+// feature row (L*F values) is read/written contiguously.
+
+#include "anr_common.h"
+
+#include <cmath>
+
+namespace anr {
+
+struct GridLevels {
+  uint32_t offset[ANR_MAX_LEVELS];
+  uint32_t size[ANR_MAX_LEVELS];  // hashmap size T_l (entries)
+  uint32_t res[ANR_MAX_LEVELS];
+  float scale[ANR_MAX_LEVELS];
+};
+
+template <int D>
+__device__ __forceinline__ uint32_t grid_index(uint32_t T, uint32_t res, const uint32_t* g) {
+  uint32_t stride = 1, index = 0;
+#pragma unroll
+  for (int d = 0; d < D && stride <= T; ++d) {
+    index += g[d] * stride;
+    stride *= res;
+  }
+  if (T < stride) {
+    constexpr uint32_t primes[3] = {1u, 2654435761u, 805459861u};
+    index = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) index ^= g[d] * primes[d];
+  }
+  return index % T;
+}
+
+template <typename T, int F>
+struct Vec;
+template <>
+struct Vec<__half, 2> {
+  __device__ static void load(const __half* p, float* v) {
+    const __half2 h = *reinterpret_cast<const __half2*>(p);
+    const float2 f = __half22float2(h);
+    v[0] = f.x;
+    v[1] = f.y;
+  }
+};
+template <>
+struct Vec<float, 2> {
+  __device__ static void load(const float* p, float* v) {
+    const float2 f = *reinterpret_cast<const float2*>(p);
+    v[0] = f.x;
+    v[1] = f.y;
+  }
+};
+template <typename T>
+struct Vec<T, 1> {
+  __device__ static void load(const T* p, float* v) { v[0] = to_f32<T>(p[0]); }
+};
+template <typename T>
+struct Vec<T, 4> {
+  __device__ static void load(const T* p, float* v) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) v[f] = to_f32<T>(p[f]);
+  }
+};
+template <typename T>
+struct Vec<T, 8> {
+  __device__ static void load(const T* p, float* v) {
+#pragma unroll
+    for (int f = 0; f < 8; ++f) v[f] = to_f32<T>(p[f]);
+  }
+};
+
+template <typename TO, int F>
+__device__ __forceinline__ void store_feat(TO* p, const float* v) {
+#pragma unroll
+  for (int f = 0; f < F; ++f) p[f] = from_f32<TO>(v[f]);
+}
+template <>
+__device__ __forceinline__ void store_feat<__half, 2>(__half* p, const float* v) {
+  *reinterpret_cast<__half2*>(p) = __floats2half2_rn(v[0], v[1]);
+}
+
+// lanes_per_chunk (16 or 32) lanes serve one chunk; lane l within the group = level l.
+template <int D, int F, typename TT, typename TO>
+__global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
+    GridLevels G, int n_levels, int lanes_per_chunk, const float* __restrict__ x,
+    int64_t x_stride, int64_t M, int64_t K, const TT* __restrict__ table,
+    TO* __restrict__ out, int64_t out_stride) {
+  const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t chunk = gtid / lanes_per_chunk;
+  const int level = static_cast<int>(gtid % lanes_per_chunk);
+  const int64_t m0 = chunk * K;
+  if (level >= n_levels || m0 >= M) return;
+  const int64_t m1 = m0 + K < M ? m0 + K : M;
+
+  const float scale = G.scale[level];
+  const uint32_t res = G.res[level];
+  const uint32_t T = G.size[level];
+  const TT* __restrict__ grid = table + static_cast<int64_t>(G.offset[level]) * F;
+
+  uint32_t cell[D];
+  bool have = false;
+#pragma unroll
+  for (int d = 0; d < D; ++d) cell[d] = 0u;
+  float val[1 << D][F];
+
+  for (int64_t m = m0; m < m1; ++m) {
+    float w[D];
+    uint32_t g[D];
+    bool same = have;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float p = fmaf(scale, x[m * x_stride + d], 0.5f);
+      const float fl = floorf(p);
+      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
+      w[d] = p - fl;
+      same = same && (g[d] == cell[d]);
+    }
+    if (!same) {
+      have = true;
+#pragma unroll
+      for (int c = 0; c < (1 << D); ++c) {
+        uint32_t gc[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) gc[d] = g[d] + ((c >> d) & 1);
+        const uint32_t idx = grid_index<D>(T, res, gc);
+        Vec<TT, F>::load(grid + static_cast<int64_t>(idx) * F, val[c]);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) cell[d] = g[d];
+    }
+    float acc[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) acc[f] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < (1 << D); ++c) {
+      float wt = 1.0f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
+#pragma unroll
+      for (int f = 0; f < F; ++f) acc[f] = fmaf(wt, val[c][f], acc[f]);
+    }
+    store_feat<TO, F>(out + m * out_stride + level * F, acc);
+  }
+}
+
+template <typename TG>
+__device__ __forceinline__ float load_grad(const TG* p) {
+  return to_f32<TG>(*p);
+}
+
+template <int D, int F, typename TG>
+__global__ void __launch_bounds__(256) hashgrid_bwd_kernel(
+    GridLevels G, int n_levels, int lanes_per_chunk, const float* __restrict__ x,
+    int64_t x_stride, int64_t M, int64_t K, const TG* __restrict__ dout,
+    int64_t dout_stride, float* __restrict__ dtable) {
+  const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t chunk = gtid / lanes_per_chunk;
+  const int level = static_cast<int>(gtid % lanes_per_chunk);
+  const int64_t m0 = chunk * K;
+  if (level >= n_levels || m0 >= M) return;
+  const int64_t m1 = m0 + K < M ? m0 + K : M;
+
+  const float scale = G.scale[level];
+  const uint32_t res = G.res[level];
+  const uint32_t T = G.size[level];
+  float* __restrict__ grad = dtable + static_cast<int64_t>(G.offset[level]) * F;
+
+  uint32_t cell[D];
+  bool have = false;
+  float acc[1 << D][F];
+#pragma unroll
+  for (int d = 0; d < D; ++d) cell[d] = 0u;
+#pragma unroll
+  for (int c = 0; c < (1 << D); ++c)
+#pragma unroll
+    for (int f = 0; f < F; ++f) acc[c][f] = 0.0f;
+
+  auto flush = [&]() {
+#pragma unroll
+    for (int c = 0; c < (1 << D); ++c) {
+      bool any = false;
+#pragma unroll
+      for (int f = 0; f < F; ++f) any = any || (acc[c][f] != 0.0f);
+      if (any) {
+        uint32_t gc[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) gc[d] = cell[d] + ((c >> d) & 1);
+        const uint32_t idx = grid_index<D>(T, res, gc);
+        float* dst = grad + static_cast<int64_t>(idx) * F;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          if (acc[c][f] != 0.0f) atomicAdd(dst + f, acc[c][f]);
+          acc[c][f] = 0.0f;
+        }
+      }
+    }
+  };
+
+  for (int64_t m = m0; m < m1; ++m) {
+    float w[D];
+    uint32_t g[D];
+    bool same = have;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float p = fmaf(scale, x[m * x_stride + d], 0.5f);
+      const float fl = floorf(p);
+      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
+      w[d] = p - fl;
+      same = same && (g[d] == cell[d]);
+    }
+    if (!same) {
+      if (have) flush();
+      have = true;
+#pragma unroll
+      for (int d = 0; d < D; ++d) cell[d] = g[d];
+    }
+    float gv[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) gv[f] = load_grad<TG>(dout + m * dout_stride + level * F + f);
+#pragma unroll
+    for (int c = 0; c < (1 << D); ++c) {
+      float wt = 1.0f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
+#pragma unroll
+      for (int f = 0; f < F; ++f) acc[c][f] = fmaf(wt, gv[f], acc[c][f]);
+    }
+  }
+  if (have) flush();
+}
+
+static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
+  if (d->n_levels < 1 || d->n_levels > ANR_MAX_LEVELS) return false;
+  for (int l = 0; l < d->n_levels; ++l) {
+    G->offset[l] = d->offsets[l];
+    G->size[l] = d->offsets[l + 1] - d->offsets[l];
+    G->res[l] = d->resolutions[l];
+    G->scale[l] = d->scales[l];
+    if (G->size[l] == 0) return false;
+  }
+  return true;
+}
+
+// Samples per chunk: long chunks amortise the per-cell gathers/atomics, but the grid
+// must still fill 256 CUs. Aim for >= 64K chunks.
+static int64_t pick_chunk(int64_t M) {
+  int64_t K = M / 65536;
+  if (K < 1) K = 1;
+  if (K > 64) K = 64;
+  return K;
+}
+
+template <int D, int F>
+static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const float* x,
+                      int64_t x_stride, int64_t M, const void* table, int32_t tdt,
+                      void* out, int32_t odt, int64_t out_stride, hipStream_t s) {
+  const int lpc = d->n_levels <= 16 ? 16 : 32;
+  const int64_t K = pick_chunk(M);
+  const int64_t chunks = ceil_div(M, K);
+  const int64_t threads = chunks * lpc;
+  const dim3 grid(static_cast<unsigned>(ceil_div(threads, 256))), block(256);
+#define ANR_HG_FWD(TT, TO)                                                                  \
+  hipLaunchKernelGGL((hashgrid_fwd_kernel<D, F, TT, TO>), grid, block, 0, s, G,             \
+                     d->n_levels, lpc, x, x_stride, M, K, static_cast<const TT*>(table),    \
+                     static_cast<TO*>(out), out_stride)
+  if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD(__half, __half);
+  else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD(__half, float);
+  else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD(float, __half);
+  else ANR_HG_FWD(float, float);
+#undef ANR_HG_FWD
+  ANR_CHECK_LAUNCH("anr_hashgrid_fwd");
+  return ANR_OK;
+}
+
+template <int D, int F>
+static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const float* x,
+                      int64_t x_stride, int64_t M, const void* dout, int32_t gdt,
+                      int64_t dout_stride, float* dtable, hipStream_t s) {
+  const int lpc = d->n_levels <= 16 ? 16 : 32;
+  const int64_t K = pick_chunk(M);
+  const int64_t chunks = ceil_div(M, K);
+  const int64_t threads = chunks * lpc;
+  const dim3 grid(static_cast<unsigned>(ceil_div(threads, 256))), block(256);
+  if (gdt == ANR_F16)
+    hipLaunchKernelGGL((hashgrid_bwd_kernel<D, F, __half>), grid, block, 0, s, G,
+                       d->n_levels, lpc, x, x_stride, M, K,
+                       static_cast<const __half*>(dout), dout_stride, dtable);
+  else
+    hipLaunchKernelGGL((hashgrid_bwd_kernel<D, F, float>), grid, block, 0, s, G,
+                       d->n_levels, lpc, x, x_stride, M, K,
+                       static_cast<const float*>(dout), dout_stride, dtable);
+  ANR_CHECK_LAUNCH("anr_hashgrid_bwd");
+  return ANR_OK;
+}
+
+}  // namespace anr
+
+extern "C" int anr_hashgrid_init(anr_hashgrid_desc* d, int32_t n_dims, int32_t n_levels,
+                                 int32_t n_features, int32_t base_resolution,
+                                 float per_level_scale, int32_t log2_hashmap_size) {
+  using namespace anr;
+  ANR_CHECK_ARG(d, "anr_hashgrid_init: null desc");
+  ANR_CHECK_ARG(n_dims == 2 || n_dims == 3, "anr_hashgrid_init: n_dims must be 2 or 3");
+  ANR_CHECK_ARG(n_levels >= 1 && n_levels <= ANR_MAX_LEVELS,
+                "anr_hashgrid_init: n_levels must be in [1, %d]", ANR_MAX_LEVELS);
+  ANR_CHECK_ARG(n_features == 1 || n_features == 2 || n_features == 4 || n_features == 8,
+                "anr_hashgrid_init: n_features must be 1, 2, 4 or 8");
+  ANR_CHECK_ARG(log2_hashmap_size >= 4 && log2_hashmap_size <= 30,
+                "anr_hashgrid_init: log2_hashmap_size out of range");
+  ANR_CHECK_ARG(base_resolution >= 1 && per_level_scale >= 1.0f,
+                "anr_hashgrid_init: bad resolution parameters");
+  memset(d, 0, sizeof(*d));
+  d->n_dims = n_dims;
+  d->n_levels = n_levels;
+  d->n_features = n_features;
+  d->base_resolution = base_resolution;
+  d->per_level_scale = per_level_scale;
+  d->log2_hashmap_size = log2_hashmap_size;
+  const float log2_pls = std::log2(per_level_scale);
+  const uint32_t max_params = 0xffffffffu / 2;
+  uint64_t offset = 0;
+  for (int l = 0; l < n_levels; ++l) {
+    const float scale =
+        std::exp2(static_cast<float>(l) * log2_pls) * static_cast<float>(base_resolution) -
+        1.0f;
+    const uint32_t res = static_cast<uint32_t>(std::ceil(scale)) + 1u;
+    uint64_t params_in_level;
+    if (std::pow(static_cast<float>(res), static_cast<float>(n_dims)) >
+        static_cast<float>(max_params)) {
+      params_in_level = max_params;
+    } else {
+      params_in_level = 1;
+      for (int k = 0; k < n_dims; ++k) params_in_level *= res;
+    }
+    params_in_level = (params_in_level + 7) / 8 * 8;
+    const uint64_t T = 1ull << log2_hashmap_size;
+    if (params_in_level > T) params_in_level = T;
+    d->scales[l] = scale;
+    d->resolutions[l] = res;
+    d->offsets[l] = static_cast<uint32_t>(offset);
+    offset += params_in_level;
+    ANR_CHECK_ARG(offset < (1ull << 32), "anr_hashgrid_init: table too large");
+  }
+  d->offsets[n_levels] = static_cast<uint32_t>(offset);
+  d->n_params = static_cast<int64_t>(offset) * n_features;
+  return ANR_OK;
+}
+
+#define ANR_HG_DISPATCH(FN, ...)                                                   \
+  switch (d->n_dims * 16 + d->n_features) {                                        \
+    case 2 * 16 + 1: return FN<2, 1>(__VA_ARGS__);                                 \
+    case 2 * 16 + 2: return FN<2, 2>(__VA_ARGS__);                                 \
+    case 2 * 16 + 4: return FN<2, 4>(__VA_ARGS__);                                 \
+    case 2 * 16 + 8: return FN<2, 8>(__VA_ARGS__);                                 \
+    case 3 * 16 + 1: return FN<3, 1>(__VA_ARGS__);                                 \
+    case 3 * 16 + 2: return FN<3, 2>(__VA_ARGS__);                                 \
+    case 3 * 16 + 4: return FN<3, 4>(__VA_ARGS__);                                 \
+    case 3 * 16 + 8: return FN<3, 8>(__VA_ARGS__);                                 \
+    default:                                                                       \
+      ::anr::set_error("hashgrid: unsupported n_dims=%d n_features=%d", d->n_dims, \
+                       d->n_features);                                             \
+      return ANR_E_UNSUPPORTED;                                                    \
+  }
+
+extern "C" int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x,
+                                int64_t x_stride, int64_t M, const void* table,
+                                int32_t table_dtype, void* out, int32_t out_dtype,
+                                int64_t out_stride, anr_stream_t stream) {
+  using namespace anr;
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(d && x && table && out, "anr_hashgrid_fwd: null argument");
+  ANR_CHECK_ARG(M >= 0 && x_stride >= d->n_dims &&
+                    out_stride >= (int64_t)d->n_levels * d->n_features,
+                "anr_hashgrid_fwd: bad shape/stride");
+  ANR_CHECK_ARG((table_dtype == ANR_F16 || table_dtype == ANR_F32) &&
+                    (out_dtype == ANR_F16 || out_dtype == ANR_F32),
+                "anr_hashgrid_fwd: bad dtype");
+  if (M == 0) return ANR_OK;
+  GridLevels G;
+  ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_fwd: descriptor not initialised");
+  ANR_HG_DISPATCH(launch_fwd, G, d, x, x_stride, M, table, table_dtype, out, out_dtype,
+                  out_stride, as_stream(stream));
+}
+
+extern "C" int anr_hashgrid_bwd(const anr_hashgrid_desc* d, const float* x,
+                                int64_t x_stride, int64_t M, const void* dout,
+                                int32_t dout_dtype, int64_t dout_stride, float* dtable,
+                                anr_stream_t stream) {
+  using namespace anr;
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(d && x && dout && dtable, "anr_hashgrid_bwd: null argument");
+  ANR_CHECK_ARG(M >= 0 && x_stride >= d->n_dims &&
+                    dout_stride >= (int64_t)d->n_levels * d->n_features,
+                "anr_hashgrid_bwd: bad shape/stride");
+  ANR_CHECK_ARG(dout_dtype == ANR_F16 || dout_dtype == ANR_F32, "anr_hashgrid_bwd: bad dtype");
+  if (M == 0) return ANR_OK;
+  GridLevels G;
+  ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_bwd: descriptor not initialised");
+  ANR_HG_DISPATCH(launch_bwd, G, d, x, x_stride, M, dout, dout_dtype, dout_stride, dtable,
+                  as_stream(stream));
+}

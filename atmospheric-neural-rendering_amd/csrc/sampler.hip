@@ -1,0 +1,192 @@
+// K1 + K2: stratified ray sampler fused with the HARP2 "horizontal" preprocessor.
+//
+// Reference semantics (file:line relative to nasa/atmospheric-neural-rendering):
+//   sample_uniform_bins   src/atmonr/samplers.py:8-47
+//   preprocess_coords     src/atmonr/datasets/harp2.py:372-386
+//   cartesian_to_horizontal (Bowring)  src/atmonr/geospatial/wgs_84.py:56-97
+//   Instant-NGP remap     src/atmonr/pipelines/instant_ngp.py:149,160
+//
+// One thread per sample. The reference runs ~30 separate fp64 elementwise passes over
+// (B,N,3); here each sample is read once (ray data is shared through L1/L2 by the 1024
+// samples of a ray) and the three outputs are written once. Each arithmetic step keeps
+// the reference's operation order and rounding points: f32 where torch computes in f32,
+// f64 where the fp64 `offset` promotes (harp2.py:376). FMA contraction is disabled so
+// the f32 parts (z, pts) are bit-identical to torch's for identical draws u.
+#pragma clang fp contract(off)
+
+#include "anr_common.h"
+
+namespace anr {
+
+// WGS-84 constants, wgs_84.py:16-20 (Python doubles).
+constexpr double kA = 6378137.0;
+constexpr double kB = 6356752.314245;
+constexpr double kE = (kA * kA - kB * kB) / (kA * kA);
+constexpr double kE2 = (kA * kA - kB * kB) / (kB * kB);
+constexpr double kPi = 3.141592653589793;  // torch.pi
+
+struct PrepDev {
+  int mode, shift_lon, ngp_remap;
+  float scale_f;  // (float)scale: torch multiplies an f32 tensor by a Python float in f32
+  double offset[3];
+  double lat_min, lat_range, lon_min, lon_range, h;
+  float alt_compress;
+};
+
+// Python-style modulus (torch.remainder for doubles): a - floor(a/b)*b.
+__device__ __forceinline__ double py_mod(double a, double b) {
+  double r = fmod(a, b);
+  if (r != 0.0 && ((r < 0.0) != (b < 0.0))) r += b;
+  return r;
+}
+
+// torch.clip(v, -1, 1): NaN propagates (fminf/fmaxf would drop it).
+__device__ __forceinline__ float clip1(float v) { return v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v); }
+
+// preprocess_coords for one point p (normalized scene frame, f32) -> coords (f32).
+__device__ __forceinline__ void preprocess_point(const PrepDev& P, float px, float py,
+                                                 float pz, float* out) {
+  float cx = px, cy = py, cz = pz;
+  if (P.mode == 1) {
+    // coords_xyz * scale (f32) + offset (f64) -> f64, harp2.py:376
+    const double x = static_cast<double>(px * P.scale_f) + P.offset[0];
+    const double y = static_cast<double>(py * P.scale_f) + P.offset[1];
+    const double z = static_cast<double>(pz * P.scale_f) + P.offset[2];
+    // cartesian_to_horizontal, wgs_84.py:83-97
+    const double lon = atan2(y, x);
+    const double D = sqrt(x * x + y * y);
+    const double u = atan2(z / D, 0.0 + kA / kB);
+    const double su = sin(u), cu = cos(u);
+    const double lat = atan2(z + (kE2 * kB) * (su * su * su), D - (kE * kA) * (cu * cu * cu));
+    const double sl = sin(lat);
+    const double Nr = kA / sqrt(1.0 - kE * (sl * sl));
+    const double alt = x / (cos(lat) * cos(lon)) - Nr;
+    double lat_d = lat * 180.0 / kPi;
+    double lon_d = lon * 180.0 / kPi;
+    if (P.shift_lon) lon_d = py_mod(lon_d, 360.0) - 180.0;  // harp2.py:379-380
+    // harp2.py:381-383
+    const double a = 2.0 * (lat_d - P.lat_min) / P.lat_range - 1.0;
+    const double b = 2.0 * (lon_d - P.lon_min) / P.lon_range - 1.0;
+    const double c = 2.0 * alt / P.h - 1.0;
+    // .to(float32) then clip(-1, 1), harp2.py:384-385
+    cx = clip1(static_cast<float>(a));
+    cy = clip1(static_cast<float>(b));
+    cz = clip1(static_cast<float>(c));
+  }
+  if (P.ngp_remap) {
+    // pts = (pts + 1) / 2 ; pts[..., 2] /= alt_compress_factor (instant_ngp.py:149,160)
+    cx = (cx + 1.0f) / 2.0f;
+    cy = (cy + 1.0f) / 2.0f;
+    cz = (cz + 1.0f) / 2.0f;
+    cz = cz / P.alt_compress;
+  }
+  out[0] = cx;
+  out[1] = cy;
+  out[2] = cz;
+}
+
+__global__ void __launch_bounds__(256) sample_uniform_bins_kernel(
+    const float* __restrict__ origin, const float* __restrict__ dir,
+    const float* __restrict__ len, const float* __restrict__ u,
+    const float* __restrict__ bins, int64_t B, int32_t N, float* __restrict__ pts,
+    float* __restrict__ zout, PrepDev P, int do_prep, float* __restrict__ coords) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= B * N) return;
+  const int64_t b = idx / N;
+  const int32_t i = static_cast<int32_t>(idx - b * N);
+  // samplers.py:42 — z = (bins[:-1] + t_in_bin / n_bins) * len
+  const float t = u ? u[idx] : 0.5f;
+  const float z = (bins[i] + t / static_cast<float>(N)) * len[b];
+  // samplers.py:45 — pts = origin + dir * z
+  const float px = origin[b * 3 + 0] + dir[b * 3 + 0] * z;
+  const float py = origin[b * 3 + 1] + dir[b * 3 + 1] * z;
+  const float pz = origin[b * 3 + 2] + dir[b * 3 + 2] * z;
+  if (zout) zout[idx] = z;
+  if (pts) {
+    pts[idx * 3 + 0] = px;
+    pts[idx * 3 + 1] = py;
+    pts[idx * 3 + 2] = pz;
+  }
+  if (do_prep) {
+    float c[3];
+    preprocess_point(P, px, py, pz, c);
+    coords[idx * 3 + 0] = c[0];
+    coords[idx * 3 + 1] = c[1];
+    coords[idx * 3 + 2] = c[2];
+  }
+}
+
+__global__ void __launch_bounds__(256) preprocess_points_kernel(
+    const float* __restrict__ pts, int64_t P_n, PrepDev P, float* __restrict__ coords) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= P_n) return;
+  float c[3];
+  preprocess_point(P, pts[idx * 3 + 0], pts[idx * 3 + 1], pts[idx * 3 + 2], c);
+  coords[idx * 3 + 0] = c[0];
+  coords[idx * 3 + 1] = c[1];
+  coords[idx * 3 + 2] = c[2];
+}
+
+static PrepDev make_prep(const anr_prep_params* p) {
+  PrepDev d{};
+  d.mode = p->mode;
+  d.shift_lon = p->shift_lon;
+  d.ngp_remap = p->ngp_remap;
+  d.scale_f = static_cast<float>(p->scale);
+  for (int k = 0; k < 3; ++k) d.offset[k] = p->offset[k];
+  d.lat_min = p->lat_min;
+  d.lat_range = p->lat_range;
+  d.lon_min = p->lon_min;
+  d.lon_range = p->lon_range;
+  d.h = p->ray_origin_height;
+  d.alt_compress = p->alt_compress;
+  return d;
+}
+
+}  // namespace anr
+
+extern "C" int anr_sample_uniform_bins(const float* origin, const float* dir,
+                                       const float* len, const float* u,
+                                       const float* bins, int64_t B, int32_t N,
+                                       float* pts, float* z, const anr_prep_params* prep,
+                                       float* coords, anr_stream_t stream) {
+  using namespace anr;
+  if (B == 0) return ANR_OK;
+  ANR_CHECK_ARG(origin && dir && len && bins, "anr_sample_uniform_bins: null ray input");
+  ANR_CHECK_ARG(B >= 0 && N > 0, "anr_sample_uniform_bins: bad shape B=%lld N=%d",
+                (long long)B, N);
+  ANR_CHECK_ARG((coords == nullptr) == (prep == nullptr),
+                "anr_sample_uniform_bins: coords and prep must be given together");
+  if (B == 0) return ANR_OK;
+  PrepDev P{};
+  if (prep) {
+    ANR_CHECK_ARG(prep->mode == 0 || prep->mode == 1, "anr_sample_uniform_bins: bad mode");
+    ANR_CHECK_ARG(prep->mode == 0 || (prep->lat_range != 0.0 && prep->lon_range != 0.0 &&
+                                      prep->ray_origin_height != 0.0),
+                  "anr_sample_uniform_bins: degenerate preprocessor ranges");
+    P = make_prep(prep);
+  }
+  const int64_t total = B * N;
+  const int threads = 256;
+  hipLaunchKernelGGL(sample_uniform_bins_kernel, dim3(ceil_div(total, threads)),
+                     dim3(threads), 0, as_stream(stream), origin, dir, len, u, bins, B, N,
+                     pts, z, P, prep ? 1 : 0, coords);
+  ANR_CHECK_LAUNCH("anr_sample_uniform_bins");
+  return ANR_OK;
+}
+
+extern "C" int anr_preprocess_points(const float* pts, int64_t P_n,
+                                     const anr_prep_params* prep, float* coords,
+                                     anr_stream_t stream) {
+  using namespace anr;
+  if (P_n == 0) return ANR_OK;
+  ANR_CHECK_ARG(pts && prep && coords, "anr_preprocess_points: null argument");
+  ANR_CHECK_ARG(P_n >= 0, "anr_preprocess_points: negative size");
+  ANR_CHECK_ARG(prep->mode == 0 || prep->mode == 1, "anr_preprocess_points: bad mode");
+  if (P_n == 0) return ANR_OK;
+  PrepDev P = make_prep(prep);
+  hipLaunchKernelGGL(preprocess_points_kernel, dim3(ceil_div(P_n, 256)), dim3(256), 0,
+                     as_stream(stream), pts, P_n, P, coords);
+  ANR_CHECK_LAUNCH("anr_preprocess_points");
+  return ANR_OK;
+}

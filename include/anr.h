@@ -1,0 +1,227 @@
+/*
+ * anr.h — C ABI of libanr_hip.so, the MI355X (gfx950) kernels behind the AtmoNR
+ * volumetric-renderer hot path.
+ *
+ * The reference (nasa/atmospheric-neural-rendering) has no C ABI: its hot path is
+ * Python glue (samplers.py, datasets/harp2.py, graphics_utils.py, losses.py) around
+ * tiny-cuda-nn's CUDA modules (tinycudann.Encoding / tinycudann.Network, bound through
+ * pybind11 at pipelines/instant_ngp.py:4,60-85,163-174,236-237). Each entry point below
+ * replaces one of those call sites; the reference line it stands in for is cited on it.
+ * The Python host (atmonr_amd/_lib.py) binds these through ctypes; INTEGRATION.md shows
+ * the binding.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer owned by the caller (torch's caching allocator);
+ *     the library allocates no device memory of its own;
+ *   - work is enqueued on `stream` (a hipStream_t, e.g. torch.cuda.current_stream()
+ *     .cuda_stream); nothing synchronises the host;
+ *   - return 0 on success, a negative ANR_E* code on error; anr_last_error() returns a
+ *     thread-local message for the last failure. Errors never throw across the ABI;
+ *   - sizes are int64; row strides are in ELEMENTS of the tensor's dtype;
+ *   - dtype codes: ANR_F32 = 0, ANR_F16 = 1.
+ */
+#ifndef ANR_H_
+#define ANR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ANR_ABI_VERSION 1
+
+enum anr_dtype { ANR_F32 = 0, ANR_F16 = 1 };
+
+enum anr_status {
+  ANR_OK = 0,
+  ANR_E_INVALID = -1,     /* bad argument (shape, dtype, unsupported config) */
+  ANR_E_LAUNCH = -2,      /* hipLaunchKernel / hipGetLastError reported an error */
+  ANR_E_UNSUPPORTED = -3  /* configuration outside the compiled kernel set */
+};
+
+typedef void* anr_stream_t; /* hipStream_t */
+
+int anr_abi_version(void);
+const char* anr_last_error(void);
+
+/* ------------------------------------------------------------------------------------
+ * K1 + K2: stratified ray sampler fused with the HARP2 "horizontal" point preprocessor.
+ * ------------------------------------------------------------------------------------
+ * anr_prep_params mirrors the closure built by HARP2Dataset.get_point_preprocessor
+ * ("horizontal"), datasets/harp2.py:357-388, plus the Instant-NGP remap of
+ * pipelines/instant_ngp.py:149,160.
+ */
+typedef struct {
+  int32_t mode;            /* 0: no preprocessing (raw normalized xyz); 1: horizontal */
+  int32_t shift_lon;       /* dateline shift, harp2.py:366-370,379-380 */
+  int32_t ngp_remap;       /* 1: out = (p+1)/2, out.z /= alt_compress (instant_ngp.py:149,160) */
+  int32_t _pad;
+  double scale;            /* dataset.scale  (Python float), harp2.py:376 */
+  double offset[3];        /* dataset.offset (float64 tensor), harp2.py:376 */
+  double lat_min, lat_range, lon_min, lon_range; /* f32 0-dim tensors, harp2.py:361-370 */
+  double ray_origin_height;                      /* harp2.py:383 */
+  float alt_compress;                            /* config alt_compress_factor */
+  float _pad2;
+} anr_prep_params;
+
+/* sample_uniform_bins (samplers.py:8-47) [+ preprocess (harp2.py:372-386)].
+ *   origin, dir: (B,3) f32; len: (B,) f32; u: (B,N) f32 uniform draws or NULL for bin
+ *   midpoints (random=False, samplers.py:37-41); bins: (N+1,) f32 = torch.linspace(0,1,N+1).
+ *   Outputs (each nullable): pts (B,N,3) f32 raw sample points (samplers.py:45);
+ *   z (B,N) f32 (samplers.py:42); coords (B,N,3) f32 preprocessed (+remapped) points.
+ *   z and pts are bit-identical to the reference for identical u (no FMA contraction). */
+int anr_sample_uniform_bins(const float* origin, const float* dir, const float* len,
+                            const float* u, const float* bins, int64_t B, int32_t N,
+                            float* pts, float* z, const anr_prep_params* prep,
+                            float* coords, anr_stream_t stream);
+
+/* preprocess_coords applied to arbitrary points (extract path, instant_ngp.py:220-233).
+ *   pts (P,3) f32 -> coords (P,3) f32. */
+int anr_preprocess_points(const float* pts, int64_t P, const anr_prep_params* prep,
+                          float* coords, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * K3 / K4: multi-resolution hash-grid encoding (tinycudann.Encoding otype "HashGrid",
+ * instant_ngp.py:60-63,163; surface 2-D grid :78-80,173).
+ * ------------------------------------------------------------------------------------ */
+#define ANR_MAX_LEVELS 32
+typedef struct {
+  int32_t n_dims;           /* 2 or 3 */
+  int32_t n_levels;         /* <= ANR_MAX_LEVELS */
+  int32_t n_features;       /* features per level: 1, 2, 4 or 8 */
+  int32_t base_resolution;
+  float per_level_scale;
+  int32_t log2_hashmap_size;
+  int64_t n_params;         /* total table entries * n_features (filled by _init) */
+  uint32_t offsets[ANR_MAX_LEVELS + 1]; /* first table entry of each level */
+  uint32_t resolutions[ANR_MAX_LEVELS];
+  float scales[ANR_MAX_LEVELS];
+} anr_hashgrid_desc;
+
+/* Fill offsets/resolutions/scales/n_params from the config (tcnn GridEncoding rules). */
+int anr_hashgrid_init(anr_hashgrid_desc* d, int32_t n_dims, int32_t n_levels,
+                      int32_t n_features, int32_t base_resolution, float per_level_scale,
+                      int32_t log2_hashmap_size);
+
+/* Forward: x (M, n_dims) f32 in [0,1] with row stride x_stride; table (n_params) in
+ * table_dtype; out (M, n_levels*n_features) written at row stride out_stride
+ * (level-major: column l*F+f), out_dtype. Interpolation accumulates in f32. */
+int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
+                     int64_t M, const void* table, int32_t table_dtype, void* out,
+                     int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
+
+/* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)
+ * f32, ACCUMULATED (caller zeroes). Duplicate corner updates inside a wavefront are
+ * pre-summed before the f32 atomics (samples along one ray share cells). */
+int anr_hashgrid_bwd(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
+                     int64_t M, const void* dout, int32_t dout_dtype, int64_t dout_stride,
+                     float* dtable, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * K5: SphericalHarmonics / Identity encodings (tinycudann Composite members,
+ * instant_ngp.py:69-72,165-169; surface :78-80).
+ * ------------------------------------------------------------------------------------ */
+/* SH of degree `degree` (1..4 -> degree^2 outputs) of x in [0,1]^3 remapped to 2x-1. */
+int anr_sh_fwd(int32_t degree, const float* x, int64_t x_stride, int64_t M, void* out,
+               int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
+/* d(SH)/dx: dout (M, degree^2) -> dx (M,3) f32, ACCUMULATED into dx. */
+int anr_sh_bwd(int32_t degree, const float* x, int64_t x_stride, int64_t M,
+               const void* dout, int32_t dout_dtype, int64_t dout_stride, float* dx,
+               int64_t dx_stride, anr_stream_t stream);
+/* Identity: out[:, :n] = x[:, :n] (dtype conversion). x may be f32 or f16. */
+int anr_identity(const void* x, int32_t x_dtype, int64_t x_stride, int64_t M, int32_t n,
+                 void* out, int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
+/* Fill out[:, :n] with a constant (tcnn pads encodings with 1.0). */
+int anr_fill_cols(void* out, int32_t out_dtype, int64_t out_stride, int64_t M, int32_t n,
+                  float value, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * K6 / K7: fully-fused MLP (tinycudann.Network otype "FullyFusedMLP",
+ * instant_ngp.py:64-68,73-77,81-85). Bias-free; ReLU hidden activation; output
+ * activation None or ReLU. Weight layout: layer k is a row-major (out_k, in_k) matrix,
+ * layers concatenated; in_0 = n_input_padded, out_last = n_output_padded.
+ * Input columns [n_input, n_input_padded) are read as 1.0 (tcnn encoding padding).
+ * ------------------------------------------------------------------------------------ */
+enum anr_activation { ANR_ACT_NONE = 0, ANR_ACT_RELU = 1 };
+typedef struct {
+  int32_t n_input, n_input_padded;   /* padded to a multiple of 16 */
+  int32_t n_output, n_output_padded; /* padded to a multiple of 16 */
+  int32_t width;                     /* 16, 32, 64 or 128 */
+  int32_t n_hidden_layers;           /* >= 1 */
+  int32_t activation;                /* ANR_ACT_RELU */
+  int32_t output_activation;         /* ANR_ACT_NONE or ANR_ACT_RELU */
+} anr_mlp_desc;
+
+int64_t anr_mlp_n_params(const anr_mlp_desc* d);
+/* Forward. precision = ANR_F16 (f16 MFMA, f32 accumulate; params_f16 used) or ANR_F32
+ * (f32 MFMA, exact f32; params_f32 used). in: (M, n_input) in_dtype; out: (M, n_output)
+ * out_dtype. */
+int anr_mlp_fwd(const anr_mlp_desc* d, int32_t precision, const void* params,
+                const void* in, int32_t in_dtype, int64_t in_stride, int64_t M, void* out,
+                int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
+/* Backward (recomputes the forward activations on chip). dout: (M, n_output);
+ * din (nullable): (M, n_input) written (not accumulated); dparams: f32, ACCUMULATED. */
+int anr_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void* params,
+                const void* in, int32_t in_dtype, int64_t in_stride, int64_t M,
+                const void* dout, int32_t dout_dtype, int64_t dout_stride, void* din,
+                int32_t din_dtype, int64_t din_stride, float* dparams,
+                anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * K8: transmittance / alpha-composite integrator, render + render_with_surface
+ * (graphics_utils.py:6-77), one wavefront per ray with shuffle prefix scans.
+ * ------------------------------------------------------------------------------------
+ * z (B,N) f32 multiplied by z_scale in f32 (instant_ngp.py:188 z_vals*(scale/1000));
+ * color (B,N,C) and sigma (B,N,S) (S = 1 or C) in io_dtype; color_surf (B,C) or NULL
+ * (plain render). Outputs (nullable unless noted): color_map (B,C) [required],
+ * color_map_atmo, color_map_surf (B,C), weights (B,N,S), alpha (B,N,S); io_dtype.
+ * Arithmetic is f32 internally. */
+int anr_composite_fwd(const float* z, float z_scale, const void* color, const void* sigma,
+                      const void* color_surf, int32_t io_dtype, int64_t B, int32_t N,
+                      int32_t C, int32_t S, void* color_map, void* color_map_atmo,
+                      void* color_map_surf, void* weights, void* alpha,
+                      anr_stream_t stream);
+/* Backward. Gradients in (nullable; io_dtype): d_color_map, d_atmo, d_surf (B,C),
+ * d_weights (B,N,S), d_alpha (B,N,S). Outputs (nullable): d_color (B,N,C),
+ * d_sigma (B,N,S), d_color_surf (B,C) (io_dtype), d_z (B,N) f32 (dL/dz before scaling
+ * by z_scale is applied, i.e. w.r.t. the unscaled z input). */
+int anr_composite_bwd(const float* z, float z_scale, const void* color, const void* sigma,
+                      const void* color_surf, int32_t io_dtype, int64_t B, int32_t N,
+                      int32_t C, int32_t S, const void* d_color_map, const void* d_atmo,
+                      const void* d_surf, const void* d_weights, const void* d_alpha,
+                      void* d_color, void* d_sigma, void* d_color_surf, float* d_z,
+                      anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * K9: losses (losses.py:5-33) on pred = take_along_dim(color_map, irgb_idx)
+ * (instant_ngp.py:259-263). Writes the scalar loss (f32) and dL/dcolor_map (B,C).
+ * ------------------------------------------------------------------------------------ */
+enum anr_loss { ANR_LOSS_DARK = 0, ANR_LOSS_HDR = 1, ANR_LOSS_L1 = 2,
+                ANR_LOSS_L1_PLUS_HDR = 3, ANR_LOSS_MSE = 4, ANR_LOSS_MSE_PLUS_HDR = 5 };
+/* color_map (B,C) pred_dtype, irgb_idx (B,) int64, gt (B,) f32. loss_out: 1 f32.
+ * grad_out (nullable): (B,C) pred_dtype, dL/dcolor_map scaled by grad_scale.
+ * workspace: >= anr_loss_workspace_bytes(B) bytes (f32 partial sums). */
+int64_t anr_loss_workspace_bytes(int64_t B);
+int anr_loss_fwd_bwd(int32_t loss_type, const void* color_map, int32_t pred_dtype,
+                     int32_t C, const int64_t* irgb_idx, const float* gt, int64_t B,
+                     float max_i, float grad_scale, float* loss_out, void* grad_out,
+                     void* workspace, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * K10: fused AdamW (torch.optim.AdamW, instant_ngp.py:120-126; Adam nerf.py:70 is
+ * weight_decay = 0, decoupled = 0) over one flat f32 parameter buffer.
+ * ------------------------------------------------------------------------------------
+ * step is the 1-based step count after increment. params_f16 (nullable) receives an
+ * f16 shadow copy of the updated params (the tcnn forward precision). If zero_grad,
+ * grad is zeroed after use (fused optimizer.zero_grad). decoupled = 1: AdamW
+ * (p *= 1 - lr*wd); decoupled = 0: Adam with L2 (g += wd*p). */
+int anr_adam_step(float* params, float* grad, float* exp_avg, float* exp_avg_sq,
+                  void* params_f16, int64_t n, float lr, float beta1, float beta2,
+                  float eps, float weight_decay, int32_t decoupled, int64_t step,
+                  int32_t zero_grad, anr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ANR_H_ */

@@ -1,0 +1,341 @@
+"""Parity of every HIP kernel against the oracle / the reference's golden vectors.
+
+Tolerances (BASELINE north_star: 1e-4 relative fp32, bit-exact for sample indices):
+  * sampler z / pts: bit-exact;
+  * preprocessor: <= 2 ulp-ish (2e-7 abs on [-1,1]) — fp64 libm differences only;
+  * exact-f32 kernels (hash grid, SH, MLP f32 MFMA, composite, loss, Adam): 1e-4 relative
+    (checked as |a-b| <= 1e-4 * max|b| + small atol);
+  * f16 kernels: compared with an oracle that rounds at the same points, 1e-2 relative.
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_path, ref_tcnn
+from tests.conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def close(a, b, rel=1e-4, atol=1e-7):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = (a - b).abs().max().item() if a.numel() else 0.0
+    tol = rel * b.abs().max().item() + atol
+    assert err <= tol, f"max err {err:.3e} > tol {tol:.3e}"
+
+
+# ------------------------------------------------------------------ K1 / K2
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
+def test_sampler_bit_exact_vs_reference(dev, tag):
+    from atmonr_amd.samplers import sample_uniform_bins
+
+    g = golden("sampler.npz")
+    batch = {k: torch.from_numpy(g[f"{tag}_{n}"]).to(dev) for k, n in
+             [("origin", "origin"), ("dir", "dir"), ("len", "len")]}
+    u = torch.from_numpy(g[f"{tag}_u"]).to(dev)
+    pts, z = sample_uniform_bins(batch, u.shape[1], u=u)
+    assert torch.equal(z.cpu(), torch.from_numpy(g[f"{tag}_z"]))
+    assert torch.equal(pts.cpu(), torch.from_numpy(g[f"{tag}_pts"]))
+    pts, z = sample_uniform_bins(batch, u.shape[1], random=False)
+    assert torch.equal(z.cpu(), torch.from_numpy(g[f"{tag}_z_mid"]))
+    assert torch.equal(pts.cpu(), torch.from_numpy(g[f"{tag}_pts_mid"]))
+
+
+def test_sampler_empty_batch(dev):
+    from atmonr_amd.samplers import sample_uniform_bins
+
+    b = {"origin": torch.zeros(0, 3, device=dev), "dir": torch.zeros(0, 3, device=dev),
+         "len": torch.zeros(0, device=dev)}
+    pts, z = sample_uniform_bins(b, 64)
+    assert pts.shape == (0, 64, 3) and z.shape == (0, 64)
+
+
+def _prep_from_golden(g, tag, remap=False, alt_compress=1.0):
+    from atmonr_amd.datasets.synthetic import PointPreprocessor
+
+    scale, lat_min, lat_range, lon_min, lon_range, h0, shift = g[f"{tag}_meta"].tolist()
+    off = g[f"{tag}_offset"].tolist()
+    pp = PointPreprocessor(scale, tuple(off), lat_min, lat_range, lon_min, lon_range, h0,
+                           bool(shift))
+    return pp, pp.params(ngp_remap=remap, alt_compress=alt_compress)
+
+
+@pytest.mark.parametrize("tag", ["std", "dateline"])
+def test_preprocessor_vs_reference(dev, tag):
+    from atmonr_amd.samplers import preprocess_points, sample_and_preprocess
+
+    g = golden("preprocess.npz")
+    pp, prm = _prep_from_golden(g, tag)
+    pts = torch.from_numpy(g[f"{tag}_pts"]).to(dev)
+    out = preprocess_points(pts, prm).cpu().numpy()
+    ref = g[f"{tag}_coords"]
+    assert np.abs(out - ref).max() <= 2e-7
+    assert (out == ref).mean() > 0.99
+    # fused sampler + preprocessor + Instant-NGP remap == op-by-op reference path
+    _, prm8 = _prep_from_golden(g, tag, remap=True, alt_compress=8.0)
+    batch = {"origin": torch.from_numpy(g[f"{tag}_ray_origin"]).to(dev),
+             "dir": torch.from_numpy(g[f"{tag}_ray_dir"]).to(dev),
+             "len": torch.from_numpy(g[f"{tag}_ray_len"]).to(dev)}
+    torch.manual_seed(7)
+    u = torch.rand(batch["origin"].shape[0], 32, device=dev)
+    _, z, coords = sample_and_preprocess(batch, 32, prm8, u=u)
+    p_ref, z_ref = ref_path.sample_uniform_bins(*(batch[k].cpu() for k in ("origin", "dir", "len")),
+                                                u.cpu(), 32)
+    assert torch.equal(z.cpu(), z_ref)
+    c_ref = torch.from_numpy(ref_path.preprocess_horizontal(
+        p_ref.numpy(), pp.scale, pp.offset, pp.lat_min, pp.lat_range, pp.lon_min, pp.lon_range,
+        pp.ray_origin_height, pp.shift_lon))
+    c_ref = (c_ref + 1) / 2
+    c_ref[..., 2] = c_ref[..., 2] / 8
+    assert (coords.cpu() - c_ref).abs().max() <= 2e-7
+
+
+# ------------------------------------------------------------------ K3 / K4
+def _grid_inputs(dev, cfg, M, coherent, seed=0):
+    gen = torch.Generator().manual_seed(seed)
+    if coherent:  # ray-like: consecutive samples along straight lines
+        R = max(1, M // 256)
+        o = torch.rand(R, 1, cfg[0], generator=gen)
+        d = (torch.rand(R, 1, cfg[0], generator=gen) - 0.5) * 0.3
+        t = torch.linspace(0, 1, 256)[None, :, None]
+        x = (o + d * t).clamp(0, 1).reshape(-1, cfg[0])[:M]
+    else:
+        x = torch.rand(M, cfg[0], generator=gen)
+    return x.contiguous()
+
+
+@pytest.mark.parametrize("cfg,M,coherent", [((3, 16, 16, 1.3819, 19), 5000, False),
+                                            ((3, 16, 16, 1.3819, 19), 8192, True),
+                                            ((3, 16, 16, 1.3819, 21), 3001, True),
+                                            ((2, 16, 16, 1.3819, 19), 4096, False),
+                                            ((3, 6, 4, 2.0, 10), 777, True)])
+def test_hashgrid_fwd_bwd_f32(dev, cfg, M, coherent):
+    from atmonr_amd import _lib
+
+    d = _lib.hashgrid_desc(cfg[0], cfg[1], 2, cfg[2], cfg[3], cfg[4])
+    gen = torch.Generator().manual_seed(1)
+    table = (torch.rand(d.n_params, generator=gen) * 2 - 1)
+    x = _grid_inputs(dev, cfg, M, coherent)
+    out = torch.empty(M, cfg[1] * 2, device=dev)
+    s = _lib.stream(dev)
+    td, xd = table.to(dev), x.to(dev)
+    _lib.call("anr_hashgrid_fwd", ctypes.byref(d), xd.data_ptr(), cfg[0], M, td.data_ptr(),
+              _lib.F32, out.data_ptr(), _lib.F32, out.stride(0), s)
+    ref = ref_tcnn.hashgrid_fwd(x.numpy(), table.numpy(), cfg)
+    close(out, ref, rel=1e-5)
+    dout = torch.randn(M, cfg[1] * 2, generator=gen)
+    dtab = torch.zeros(d.n_params, device=dev)
+    dd = dout.to(dev)
+    _lib.call("anr_hashgrid_bwd", ctypes.byref(d), xd.data_ptr(), cfg[0], M, dd.data_ptr(),
+              _lib.F32, dd.stride(0), dtab.data_ptr(), s)
+    gref = ref_tcnn.hashgrid_bwd(x.numpy(), dout.numpy(), cfg, d.n_params // 2)
+    close(dtab, gref, rel=1e-5, atol=1e-5)
+
+
+def test_hashgrid_f16_table_and_strided_output(dev):
+    from atmonr_amd import _lib
+
+    cfg = (3, 16, 16, 1.3819, 19)
+    d = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, 19)
+    gen = torch.Generator().manual_seed(2)
+    table = ((torch.rand(d.n_params, generator=gen) * 2 - 1) * 1e-2).half()
+    M = 4000
+    x = _grid_inputs(dev, cfg, M, True, seed=3)
+    big = torch.full((M, 40), -7.0, device=dev, dtype=torch.float16)  # write cols 4..35
+    xd = x.to(dev)
+    _lib.call("anr_hashgrid_fwd", ctypes.byref(d), xd.data_ptr(), 3, M, table.to(dev).data_ptr(),
+              _lib.F16, big.data_ptr() + 4 * 2, _lib.F16, 40, _lib.stream(dev))
+    ref = ref_tcnn.hashgrid_fwd(x.numpy(), table.float().numpy(), cfg)
+    close(big[:, 4:36].float(), ref, rel=2e-3, atol=1e-5)
+    assert torch.all(big[:, :4] == -7) and torch.all(big[:, 36:] == -7)
+
+
+# ------------------------------------------------------------------ K5
+@pytest.mark.parametrize("degree", [1, 2, 3, 4])
+def test_sh_fwd_bwd(dev, degree):
+    from atmonr_amd import _lib
+
+    gen = torch.Generator().manual_seed(degree)
+    M = 1000
+    x = torch.rand(M, 3, generator=gen)
+    out = torch.empty(M, degree * degree, device=dev)
+    xd = x.to(dev)
+    s = _lib.stream(dev)
+    _lib.call("anr_sh_fwd", degree, xd.data_ptr(), 3, M, out.data_ptr(), _lib.F32,
+              out.stride(0), s)
+    close(out, ref_tcnn.sh(x.numpy(), degree), rel=1e-6, atol=1e-6)
+    dout = torch.randn(M, degree * degree, generator=gen)
+    dx = torch.zeros(M, 3, device=dev)
+    _lib.call("anr_sh_bwd", degree, xd.data_ptr(), 3, M, dout.to(dev).data_ptr(), _lib.F32,
+              degree * degree, dx.data_ptr(), 3, s)
+    xx = x.double().requires_grad_(True)
+    sh = torch.from_numpy(ref_tcnn.sh(x.numpy(), degree))  # value check only
+    # autograd of the same polynomial in torch for the gradient
+    X, Y, Z = (xx * 2 - 1).unbind(1)
+    terms = [torch.full_like(X, 0.28209479177387814)]
+    if degree > 1:
+        c = 0.48860251190291987
+        terms += [-c * Y, c * Z, -c * X]
+    if degree > 2:
+        terms += [1.0925484305920792 * X * Y, -1.0925484305920792 * Y * Z,
+                  0.94617469575755997 * Z * Z - 0.31539156525251999,
+                  -1.0925484305920792 * X * Z, 0.54627421529603959 * (X * X - Y * Y)]
+    if degree > 3:
+        terms += [0.59004358992664352 * Y * (-3.0 * X * X + Y * Y),
+                  2.8906114426405538 * X * Y * Z, 0.45704579946446572 * Y * (1.0 - 5.0 * Z * Z),
+                  0.3731763325901154 * Z * (5.0 * Z * Z - 3.0),
+                  0.45704579946446572 * X * (1.0 - 5.0 * Z * Z),
+                  1.4453057213202769 * Z * (X * X - Y * Y),
+                  0.59004358992664352 * X * (-X * X + 3.0 * Y * Y)]
+    tt = torch.stack(terms, 1)
+    assert torch.allclose(tt.detach(), sh)
+    (tt * dout.double()).sum().backward()
+    close(dx, xx.grad, rel=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------ K6 / K7
+MLP_CASES = [(32, 16, 32, 1, False), (32, 16, 64, 1, False), (19, 4, 32, 2, True),
+             (19, 4, 64, 2, False), (36, 4, 32, 2, False), (16, 3, 16, 3, False),
+             (40, 20, 128, 1, True)]
+
+
+@pytest.mark.parametrize("n_in,n_out,width,n_hidden,out_relu", MLP_CASES)
+@pytest.mark.parametrize("half", [False, True])
+def test_mlp_fwd_bwd(dev, n_in, n_out, width, n_hidden, out_relu, half):
+    from atmonr_amd import _lib
+
+    d = _lib.mlp_desc(n_in, n_out, width, n_hidden, out_relu)
+    nparam = _lib.load().anr_mlp_n_params(ctypes.byref(d))
+    gen = torch.Generator().manual_seed(width + n_in)
+    params = torch.randn(nparam, generator=gen) * (1.0 / width) ** 0.5
+    M = 1001  # not a multiple of the 16-row tile
+    x = torch.randn(M, n_in, generator=gen)
+    dt = torch.float16 if half else torch.float32
+    prec = _lib.F16 if half else _lib.F32
+    s = _lib.stream(dev)
+    pd = params.to(dev).to(dt)
+    xd = x.to(dev).to(dt)
+    out = torch.empty(M, n_out, device=dev, dtype=torch.float32)
+    _lib.call("anr_mlp_fwd", ctypes.byref(d), prec, pd.data_ptr(), xd.data_ptr(),
+              _lib.dtype_code(dt), n_in, M, out.data_ptr(), _lib.F32, n_out, s)
+    xr = x.double().requires_grad_(True)
+    pr = params.double().requires_grad_(True)
+    ref = ref_tcnn.mlp_fwd(xr, pr, n_in, n_out, width, n_hidden, out_relu, half=half)
+    rel = 1e-2 if half else 1e-4
+    close(out, ref.detach(), rel=rel, atol=1e-6)
+    dout = torch.randn(M, n_out, generator=gen) * 1e-3
+    ref.backward(dout.double())
+    dparams = torch.zeros(nparam, device=dev)
+    din = torch.empty(M, n_in, device=dev, dtype=torch.float32)
+    dd = dout.to(dev)
+    _lib.call("anr_mlp_bwd", ctypes.byref(d), prec, pd.data_ptr(), xd.data_ptr(),
+              _lib.dtype_code(dt), n_in, M, dd.data_ptr(), _lib.F32, n_out, din.data_ptr(),
+              _lib.F32, n_in, dparams.data_ptr(), s)
+    close(din, xr.grad, rel=rel * 2, atol=1e-8)
+    close(dparams, pr.grad, rel=rel * 2, atol=1e-8)
+
+
+# ------------------------------------------------------------------ K8
+@pytest.mark.parametrize("tag", ["f32", "f32long", "f32multi", "f16"])
+def test_composite_vs_reference(dev, tag):
+    from atmonr_amd.graphics_utils import render, render_with_surface
+
+    g = golden("render.npz")
+    dt = torch.float16 if tag == "f16" else torch.float32
+    t = {k: torch.from_numpy(g[f"{tag}_{k}"]) for k in
+         ("z", "color", "sigma", "cs", "gcm", "gatmo", "gsurf", "gw")}
+    z = t["z"].to(dev).requires_grad_(True)
+    c = t["color"].to(dev).to(dt).requires_grad_(True)
+    s = t["sigma"].to(dev).to(dt).requires_grad_(True)
+    cs = t["cs"].to(dev).to(dt).requires_grad_(True)
+    cm, alpha, w, atmo, surf = render_with_surface(z, c, s, cs)
+    rel = 1e-4 if dt == torch.float32 else 2e-2
+    atol = 1e-6 if dt == torch.float32 else 2e-2
+    for name, out in [("cm", cm), ("alpha", alpha), ("w", w), ("atmo", atmo), ("surf", surf)]:
+        close(out.float(), torch.from_numpy(g[f"{tag}_{name}"]), rel=rel, atol=atol)
+    loss = ((cm.float() * t["gcm"].to(dev).float()).sum() + (atmo.float() * t["gatmo"].to(dev)).sum()
+            + (surf.float() * t["gsurf"].to(dev)).sum() + (w.float() * t["gw"].to(dev)).sum())
+    loss.backward()
+    if dt == torch.float32:
+        for name, ten in [("dcolor", c), ("dsigma", s), ("dcs", cs), ("dz", z)]:
+            close(ten.grad.float(), torch.from_numpy(g[f"{tag}_{name}"]), rel=1e-4, atol=1e-5)
+    cm2, _, w2 = render(t["z"].to(dev), t["color"].to(dev).to(dt), t["sigma"].to(dev).to(dt))
+    close(cm2.float(), torch.from_numpy(g[f"{tag}_plain_cm"]), rel=rel, atol=atol)
+
+
+def test_composite_known_answers(dev):
+    from atmonr_amd.graphics_utils import render_with_surface
+
+    B, N = 3, 100
+    z = torch.linspace(0, 10, N, device=dev)[None].expand(B, N).contiguous()
+    color = torch.rand(B, N, 4, device=dev)
+    cs = torch.rand(B, 4, device=dev)
+    # zero density: C = C_surf exactly
+    cm, _, w, atmo, surf = render_with_surface(z, color, torch.zeros(B, N, 1, device=dev), cs)
+    assert torch.all(w == 0) and torch.all(atmo == 0)
+    assert torch.equal(cm, cs)
+    # uniform density sigma: transmittance to the surface is exp(-sigma * z_end)
+    sig = 0.07
+    cm, _, w, atmo, surf = render_with_surface(z, torch.ones_like(color),
+                                               torch.full((B, N, 1), sig, device=dev), cs)
+    T = torch.exp(torch.tensor(-sig * 10.0))
+    close(surf, (T * cs.cpu()), rel=1e-5)
+    close(atmo, torch.full((B, 4), 1 - T.item()), rel=1e-5)
+
+
+# ------------------------------------------------------------------ K9
+@pytest.mark.parametrize("name", ["dark", "hdr", "l1", "l1_plus_hdr", "mse", "mse_plus_hdr"])
+def test_losses_vs_reference(dev, name):
+    from atmonr_amd import losses
+
+    g = golden("losses.npz")
+    p = torch.from_numpy(g["pred"]).to(dev).requires_grad_(True)
+    val = losses.LOSSES[name](p, torch.from_numpy(g["gt"]).to(dev), float(g["max_i"]))
+    val.backward()
+    close(val.detach(), torch.tensor(g[f"{name}_val"]), rel=1e-5)
+    close(p.grad, torch.from_numpy(g[f"{name}_grad"]), rel=1e-4, atol=1e-9)
+
+
+def test_indexed_loss_matches_take_along_dim(dev):
+    from atmonr_amd.losses import indexed_loss
+
+    gen = torch.Generator().manual_seed(5)
+    B = 3000
+    cm = (torch.rand(B, 4, generator=gen) * 20).to(dev).requires_grad_(True)
+    idx = torch.randint(0, 4, (B,), generator=gen).to(dev)
+    gt = (torch.rand(B, generator=gen) * 20).to(dev)
+    val = indexed_loss("mse_plus_hdr", cm, idx, gt, 25.0)
+    val.backward()
+    cr = cm.detach().cpu().double().requires_grad_(True)
+    pr = torch.take_along_dim(cr, idx.cpu()[:, None], 1)[:, 0]
+    ref = ref_path.LOSSES["mse_plus_hdr"](pr, gt.cpu().double(), 25.0)
+    ref.backward()
+    close(val.detach(), ref.detach(), rel=1e-5)
+    close(cm.grad, cr.grad, rel=1e-4, atol=1e-10)
+
+
+# ------------------------------------------------------------------ K10
+@pytest.mark.parametrize("decoupled,wd", [(True, 1e-2), (True, 0.0), (False, 1e-3)])
+def test_adam_matches_torch(dev, decoupled, wd):
+    from atmonr_amd.optim import FusedAdam
+
+    gen = torch.Generator().manual_seed(9)
+    p0 = torch.randn(10007, generator=gen)
+    grads = [torch.randn(10007, generator=gen) * 0.1 for _ in range(5)]
+    pa = torch.nn.Parameter(p0.clone().to(dev))
+    pb = torch.nn.Parameter(p0.clone())
+    kw = dict(lr=1e-2, betas=(0.9, 0.99), eps=1e-15, weight_decay=wd)
+    oa = FusedAdam([pa], decoupled=decoupled, **kw)
+    ob = (torch.optim.AdamW if decoupled else torch.optim.Adam)([pb], foreach=False, **kw)
+    for gr in grads:
+        pa.grad = gr.to(dev)
+        pb.grad = gr.clone()
+        oa.step()
+        ob.step()
+    close(pa.detach(), pb.detach(), rel=1e-5, atol=1e-6)
+    close(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"], rel=1e-5, atol=1e-12)

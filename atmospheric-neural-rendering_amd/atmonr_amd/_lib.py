@@ -159,6 +159,34 @@ _SIGNATURES = {
 }
 
 _lib = None
+_timer = None  # optional KernelTimer: HIP events around every entry-point call
+
+
+class KernelTimer:
+    """Records a (start, end) torch.cuda.Event pair on the current stream around each
+    libanr_hip call, keyed by entry-point name (bench.py's per-kernel timing)."""
+
+    def __init__(self):
+        self.events: dict[str, list] = {}
+
+    def __enter__(self):
+        global _timer
+        _timer = self
+        return self
+
+    def __exit__(self, *exc):
+        global _timer
+        _timer = None
+
+    def summary(self) -> dict[str, dict]:
+        """name -> {launches, total_ms, avg_ms}; synchronizes."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, evs in self.events.items():
+            ts = [a.elapsed_time(b) for a, b in evs]
+            out[name] = {"launches": len(ts), "total_ms": sum(ts),
+                         "avg_ms": sum(ts) / max(1, len(ts))}
+        return out
 
 
 def load() -> ctypes.CDLL:
@@ -184,10 +212,19 @@ def symbols() -> list[str]:
     return list(_SIGNATURES)
 
 
-def call(name: str, *args) -> int:
-    """Call an entry point; raise ANRError on a non-zero status."""
+def call(name: str, *args, tag: str | None = None) -> int:
+    """Call an entry point; raise ANRError on a non-zero status. ``tag`` names the call
+    for the KernelTimer (defaults to the entry-point name)."""
     lib = load()
-    rc = getattr(lib, name)(*args)
+    if _timer is not None:
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        rc = getattr(lib, name)(*args)
+        b.record()
+        _timer.events.setdefault(tag or name, []).append((a, b))
+    else:
+        rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.anr_last_error().decode(errors="replace")
         raise ANRError(f"{name} failed (status {rc}): {msg}")

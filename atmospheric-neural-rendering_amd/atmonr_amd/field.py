@@ -43,11 +43,12 @@ class IngpFieldFn(torch.autograd.Function):
 
         enc = torch.empty(M, grid.n_out, device=dev, dtype=enc_mod.dtype)
         call("anr_hashgrid_fwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(t_hash),
-             dtype_code(t_hash.dtype), ptr(enc), dtype_code(enc.dtype), enc.stride(0), s)
+             dtype_code(t_hash.dtype), ptr(enc), dtype_code(enc.dtype), enc.stride(0), s,
+             tag="hash_fwd")
         pos_out = torch.empty(M, pos_mod.n_output_dims, device=dev, dtype=torch.float32)
         call("anr_mlp_fwd", ctypes.byref(pos_mod.desc), prec, ptr(w_pos), ptr(enc),
              dtype_code(enc.dtype), enc.stride(0), M, ptr(pos_out), _lib.F32,
-             pos_out.stride(0), s)
+             pos_out.stride(0), s, tag="pos_mlp_fwd")
         # dir encoding input: [SH(dir) | pos_out[:, 1:]]  (19 columns, tcnn pads to 32)
         n_sh = dir_mod.n_output_dims - (pos_mod.n_output_dims - 1)
         dir_in = torch.empty(M, dir_mod.n_output_dims, device=dev, dtype=cdt)
@@ -60,7 +61,8 @@ class IngpFieldFn(torch.autograd.Function):
              dtype_code(cdt), dir_in.stride(0), s)
         color = torch.empty(M, dmlp.n_output_dims, device=dev, dtype=torch.float32)
         call("anr_mlp_fwd", ctypes.byref(pipe._dir_desc_relu), prec, ptr(w_dir), ptr(dir_in),
-             dtype_code(cdt), dir_in.stride(0), M, ptr(color), _lib.F32, color.stride(0), s)
+             dtype_code(cdt), dir_in.stride(0), M, ptr(color), _lib.F32, color.stride(0), s,
+             tag="dir_mlp_fwd")
         sigma = torch.relu(pos_out[:, 0])
         ctx.save_for_backward(coords, enc, pos_out, dir_in, t_hash, w_pos, w_dir)
         ctx.pipe = pipe
@@ -86,7 +88,8 @@ class IngpFieldFn(torch.autograd.Function):
         d_dir_in = torch.empty(M, dir_in.shape[1], device=dev, dtype=torch.float32)
         call("anr_mlp_bwd", ctypes.byref(pipe._dir_desc_relu), prec, ptr(w_dir), ptr(dir_in),
              dtype_code(dir_in.dtype), dir_in.stride(0), M, ptr(d_color), _lib.F32,
-             d_color.stride(0), ptr(d_dir_in), _lib.F32, d_dir_in.stride(0), ptr(g_dir), s)
+             d_color.stride(0), ptr(d_dir_in), _lib.F32, d_dir_in.stride(0), ptr(g_dir), s,
+             tag="dir_mlp_bwd")
         d_pos_out = torch.empty_like(pos_out)
         d_pos_out[:, 1:] = d_dir_in[:, ctx.n_sh:]
         if d_sigma is None:
@@ -96,7 +99,8 @@ class IngpFieldFn(torch.autograd.Function):
         d_enc = torch.empty(M, enc.shape[1], device=dev, dtype=torch.float32)
         call("anr_mlp_bwd", ctypes.byref(pos_mod.desc), prec, ptr(w_pos), ptr(enc),
              dtype_code(enc.dtype), enc.stride(0), M, ptr(d_pos_out), _lib.F32,
-             d_pos_out.stride(0), ptr(d_enc), _lib.F32, d_enc.stride(0), ptr(g_pos), s)
+             d_pos_out.stride(0), ptr(d_enc), _lib.F32, d_enc.stride(0), ptr(g_pos), s,
+             tag="pos_mlp_bwd")
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
-             _lib.F32, d_enc.stride(0), ptr(g_hash), s)
+             _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
         return None, None, None, g_hash, g_pos, g_dir, None

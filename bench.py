@@ -1,0 +1,247 @@
+"""Train-step throughput of the AtmoNR Instant-NGP hot path on MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[2]): configs/instant_ngp.json with a 16-level T=2^19
+hash grid and 2x64 fused MLPs, B = 8192 rays x N = 1024 samples per rank per step, on a
+synthetic 90-view 512x512 HARP2-shaped scene (no L1B granule exists offline). One step =
+batch gather -> fused sampler/preprocessor -> hash grid -> MLPs -> composite -> loss ->
+backward -> [RCCL all-reduce of the flat gradient when N > 1] -> fused AdamW.
+Data parallel over rays, one process per GPU, weak scaling (8192 rays per rank).
+
+Rank 0 prints ONE JSON line. ``roofline`` is for the kernel that takes the most time per
+step, timed with HIP events on the launch stream inside the timed region; its
+algorithmic bytes per sample are defined in DESIGN.md. ``cpu_baseline`` times the
+oracle's CPU restatement of the configs/nerf.json train step (rank 0, N = 1 only).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "atmospheric-neural-rendering_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_F16_PEAK_TF = 2500.0  # dense fp16/bf16 MFMA (spec, no sparsity)
+
+# Algorithmic work per unit. Hash grid, L=16 levels, F=2, D=3:
+#   fwd: 12 B coords + 16*8*2*2 B f16 corner features + 32*2 B f16 output = 588 B/sample
+#   bwd: 12 B coords + 32*4 B f32 dL/dfeature + 16*8*2*4 B f32 gradient read+write
+#        (read-modify-write) = 12 + 128 + 2048 = 2188 B/sample
+UNIT_BYTES = {"hash_fwd": 588.0, "hash_bwd": 2188.0}
+
+
+def mlp_flops_per_sample(pipe) -> dict:
+    def f(desc):
+        dims = ([desc.n_input_padded] + [desc.width] * desc.n_hidden_layers
+                + [desc.n_output_padded])
+        return 2.0 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    pos, dirm = f(pipe.pos_mlp.desc), f(pipe.dir_mlp.desc)
+    # fwd = 1x; bwd = recompute fwd + dIn + dW = 3x
+    return {"pos_mlp_fwd": pos, "dir_mlp_fwd": dirm, "pos_mlp_bwd": 3 * pos,
+            "dir_mlp_bwd": 3 * dirm}
+
+
+def ingp_config(variant: str, n_samples: int) -> dict:
+    import __graft_entry__ as ge
+
+    cfg = ge._ingp_config(n_samples)
+    ingp = cfg["instant_ngp"]
+    if variant == "committed":  # configs/instant_ngp.json as committed: T=2^21, width 32
+        ingp["encoding"]["log2_hashmap_size"] = 21
+        for k in ("network", "rgb_network", "surface_network"):
+            ingp[k]["n_neurons"] = 32
+    return cfg
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8192, help="rays per rank per step")
+    ap.add_argument("--samples", type=int, default=1024)
+    ap.add_argument("--views", type=int, default=90)
+    ap.add_argument("--img-size", type=int, default=512)
+    ap.add_argument("--variant", choices=["baseline", "committed"], default="baseline")
+    ap.add_argument("--dtype", choices=["f16", "f32"], default="f16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-kernel-timer", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from atmonr_amd import _lib
+    from atmonr_amd.batch_loader import BatchLoader
+    from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
+    from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
+
+    t0 = time.time()
+    ds = SyntheticHARP2Dataset(n_views=args.views, img_size=args.img_size, device=dev, seed=0)
+    torch.cuda.synchronize()
+    t_scene = time.time() - t0
+    cfg = ingp_config(args.variant, args.samples)
+    dtype = torch.float16 if args.dtype == "f16" else torch.float32
+    pipe = InstantNGPPipeline(cfg, ds, dtype=dtype, fused=True, seed=1337)
+    pipe.send_tensors_to(dev)
+    opt_cfg = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
+    opt = pipe.get_optimizer(opt_cfg)
+
+    # one flat f32 gradient bucket; every param's .grad is a view into it, so backward
+    # accumulates in place and DP needs exactly one all-reduce per step
+    params = [p for g in opt.param_groups for p in g["params"]]
+    n_total = sum(p.numel() for p in params)
+    flat = torch.zeros(n_total, device=dev)
+    off = 0
+    for p in params:
+        p.grad = flat[off:off + p.numel()].view_as(p)
+        off += p.numel()
+
+    loader = BatchLoader(ds, args.batch, shuffle=True, rank=rank, world_size=world, seed=0)
+    it = iter(loader)
+
+    def next_batch():
+        nonlocal it
+        try:
+            return next(it)
+        except StopIteration:
+            it = iter(loader)
+            return next(it)
+
+    def step():
+        batch = next_batch()
+        res = pipe.forward(batch)
+        loss = pipe.compute_loss(batch, res)
+        flat.zero_()
+        loss.backward()
+        if world > 1:
+            dist.all_reduce(flat, op=dist.ReduceOp.AVG)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    timer = _lib.KernelTimer() if not args.no_kernel_timer else None
+    t_start = time.perf_counter()
+    if timer:
+        with timer:
+            for _ in range(args.steps):
+                loss = step()
+    else:
+        for _ in range(args.steps):
+            loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    final_loss = float(loss.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    rays_total = args.batch * world * args.steps
+    value = rays_total / elapsed
+
+    kernels, roofline = {}, None
+    if timer:
+        summ = timer.summary()
+        flops = mlp_flops_per_sample(pipe)
+        M = args.batch * args.samples
+        for name, s in sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"]):
+            entry = {"avg_ms": round(s["avg_ms"], 4),
+                     "ms_per_step": round(s["total_ms"] / args.steps, 4)}
+            if name in UNIT_BYTES:
+                gbs = UNIT_BYTES[name] * M / (s["avg_ms"] * 1e-3) / 1e9
+                entry.update(bound="hbm", achieved=round(gbs, 1),
+                             frac=round(gbs / HBM_PEAK_GBS, 4))
+            elif name in flops:
+                tf = flops[name] * M / (s["avg_ms"] * 1e-3) / 1e12
+                entry.update(bound="mfma", achieved=round(tf, 2),
+                             frac=round(tf / MFMA_F16_PEAK_TF, 4))
+            kernels[name] = entry
+        dominant = next((n for n in kernels if "bound" in kernels[n]), None)
+        if dominant:
+            k = kernels[dominant]
+            roofline = {"kernel": dominant, "bound": k["bound"], "achieved": k["achieved"],
+                        "peak": HBM_PEAK_GBS if k["bound"] == "hbm" else MFMA_F16_PEAK_TF,
+                        "unit": "GB/s" if k["bound"] == "hbm" else "TFLOP/s",
+                        "frac": k["frac"], "traffic": None,
+                        "avg_ms": k["avg_ms"], "units_per_launch": M}
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                try:
+                    data = json.load(open(pmc))
+                    key = f"{dominant}:{args.variant}:{args.batch}x{args.samples}"
+                    roofline["traffic"] = data.get(key)
+                except (OSError, ValueError):
+                    pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline
+
+        cpu = cpu_baseline.run(budget_s=args.cpu_budget)
+
+    if rank == 0:
+        T = 2 ** cfg["instant_ngp"]["encoding"]["log2_hashmap_size"]
+        width = cfg["instant_ngp"]["network"]["n_neurons"]
+        line = {
+            "metric": "train-step rays/sec",
+            "value": round(value, 1),
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f16" if dtype == torch.float16 else "f32",
+            "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} "
+                    f"HARP2-shaped scene, {len(ds)} rays; random-init weights)",
+            "config": {
+                "workload": (f"instant_ngp {'BASELINE configs[2]' if args.variant == 'baseline' else 'committed configs/instant_ngp.json'}"
+                             f": 16-level T=2^{T.bit_length() - 1} hash grid, 2x{width} fused "
+                             f"MLP, {args.samples} samples/ray, full train step "
+                             f"(fwd+loss+bwd+AdamW)"),
+                "global_batch": args.batch * world,
+                "samples_per_ray": args.samples,
+                "parallelism": f"dp{world}",
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+            "final_loss": round(final_loss, 6),
+            "scene_build_s": round(t_scene, 2),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

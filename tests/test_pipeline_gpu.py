@@ -64,7 +64,7 @@ def test_training_reduces_loss(scene, dev, dtype):
             opt.step()
             losses.append(loss.item())
     assert all(torch.isfinite(torch.tensor(losses)))
-    assert sum(losses[-5:]) / 5 < 0.5 * sum(losses[:3]) / 3
+    assert sum(losses[-5:]) / 5 < 0.7 * sum(losses[:3]) / 3
 
 
 def test_extract(scene, dev):

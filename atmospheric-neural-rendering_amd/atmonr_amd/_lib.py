@@ -125,6 +125,7 @@ _SIGNATURES = {
     ),
     "anr_fill_cols": (c_int32, [_P, c_int32, c_int64, c_int64, c_int32, c_float, _P]),
     "anr_mlp_n_params": (c_int64, [POINTER(MlpDesc)]),
+    "anr_mlp_force_generic": (c_int32, [c_int32]),
     "anr_mlp_fwd": (
         c_int32,
         [POINTER(MlpDesc), c_int32, _P, _P, c_int32, c_int64, c_int64, _P, c_int32, c_int64, _P],

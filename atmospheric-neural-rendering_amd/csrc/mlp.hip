@@ -21,6 +21,7 @@
 #include "anr_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace anr {
 
@@ -401,7 +402,25 @@ static int grid_for(int64_t M, int waves, int max_blocks) {
 
 constexpr size_t kLdsBudget = 160 * 1024;
 
+int mlp_fused_try(const anr_mlp_desc* d, int32_t precision, bool bwd, const void* params,
+                  const void* in, int32_t in_dt, int64_t in_stride, int64_t M,
+                  const void* dout, int32_t dout_dt, int64_t dout_stride, void* out,
+                  int32_t out_dt, int64_t out_stride, float* dparams, hipStream_t st);
+
+// ANR_MLP_GENERIC=1 (or anr_mlp_force_generic) forces the generic kernels.
+static int g_force_generic = [] {
+  const char* e = getenv("ANR_MLP_GENERIC");
+  return (e && e[0] == '1') ? 1 : 0;
+}();
+static bool force_generic() { return g_force_generic != 0; }
+
 }  // namespace anr
+
+extern "C" int anr_mlp_force_generic(int32_t on) {
+  const int prev = anr::g_force_generic;
+  anr::g_force_generic = on ? 1 : 0;
+  return prev;
+}
 
 extern "C" int64_t anr_mlp_n_params(const anr_mlp_desc* d) {
   if (anr::check_desc(d) != ANR_OK) return -1;
@@ -420,6 +439,12 @@ extern "C" int anr_mlp_fwd(const anr_mlp_desc* d, int32_t precision, const void*
   ANR_CHECK_ARG(M >= 0 && in_stride >= d->n_input && out_stride >= d->n_output,
                 "anr_mlp_fwd: bad shape/stride");
   if (M == 0) return ANR_OK;
+  if (!force_generic() &&
+      mlp_fused_try(d, precision, false, params, in, in_dtype, in_stride, M, nullptr, 0, 0,
+                    out, out_dtype, out_stride, nullptr, as_stream(stream)) == 0) {
+    ANR_CHECK_LAUNCH("anr_mlp_fwd(fused)");
+    return ANR_OK;
+  }
   MlpArgs a = base_args(d, M);
   a.params = params;
   a.in = in;
@@ -465,6 +490,12 @@ extern "C" int anr_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void*
                     (din == nullptr || din_stride >= d->n_input),
                 "anr_mlp_bwd: bad shape/stride");
   if (M == 0) return ANR_OK;
+  if (!force_generic() &&
+      mlp_fused_try(d, precision, true, params, in, in_dtype, in_stride, M, dout, dout_dtype,
+                    dout_stride, din, din_dtype, din_stride, dparams, as_stream(stream)) == 0) {
+    ANR_CHECK_LAUNCH("anr_mlp_bwd(fused)");
+    return ANR_OK;
+  }
   MlpArgs a = base_args(d, M);
   a.params = params;
   a.in = in;

@@ -154,6 +154,9 @@ typedef struct {
 } anr_mlp_desc;
 
 int64_t anr_mlp_n_params(const anr_mlp_desc* d);
+/* Force the generic (shape-agnostic) MLP kernels instead of the compile-time specialised
+ * ones (on != 0). Test hook; process-wide. Returns the previous setting. */
+int anr_mlp_force_generic(int32_t on);
 /* Forward. precision = ANR_F16 (f16 MFMA, f32 accumulate; params_f16 used) or ANR_F32
  * (f32 MFMA, exact f32; params_f32 used). in: (M, n_input) in_dtype; out: (M, n_output)
  * out_dtype. */

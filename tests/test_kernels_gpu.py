@@ -203,13 +203,22 @@ def test_sh_fwd_bwd(dev, degree):
 
 # ------------------------------------------------------------------ K6 / K7
 MLP_CASES = [(32, 16, 32, 1, False), (32, 16, 64, 1, False), (19, 4, 32, 2, True),
-             (19, 4, 64, 2, False), (36, 4, 32, 2, False), (16, 3, 16, 3, False),
-             (40, 20, 128, 1, True)]
+             (19, 4, 64, 2, False), (36, 4, 32, 2, False), (36, 4, 64, 2, True),
+             (16, 3, 16, 3, False), (40, 20, 128, 1, True), (10, 16, 64, 2, False)]
+
+
+@pytest.fixture(params=["specialised", "generic"])
+def mlp_path(request):
+    from atmonr_amd import _lib
+
+    prev = _lib.load().anr_mlp_force_generic(1 if request.param == "generic" else 0)
+    yield request.param
+    _lib.load().anr_mlp_force_generic(prev)
 
 
 @pytest.mark.parametrize("n_in,n_out,width,n_hidden,out_relu", MLP_CASES)
 @pytest.mark.parametrize("half", [False, True])
-def test_mlp_fwd_bwd(dev, n_in, n_out, width, n_hidden, out_relu, half):
+def test_mlp_fwd_bwd(dev, mlp_path, n_in, n_out, width, n_hidden, out_relu, half):
     from atmonr_amd import _lib
 
     d = _lib.mlp_desc(n_in, n_out, width, n_hidden, out_relu)

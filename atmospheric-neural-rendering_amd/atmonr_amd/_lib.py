@@ -114,6 +114,7 @@ _SIGNATURES = {
         c_int32,
         [POINTER(HashGridDesc), _P, c_int64, c_int64, _P, c_int32, c_int64, _P, _P],
     ),
+    "anr_hashgrid_force_v1": (c_int32, [c_int32]),
     "anr_sh_fwd": (c_int32, [c_int32, _P, c_int64, c_int64, _P, c_int32, c_int64, _P]),
     "anr_sh_bwd": (
         c_int32,
@@ -137,6 +138,7 @@ _SIGNATURES = {
             c_int64, _P, c_int32, c_int64, _P, _P,
         ],
     ),
+    "anr_composite_force_generic": (c_int32, [c_int32]),
     "anr_composite_fwd": (
         c_int32,
         [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, c_int32,

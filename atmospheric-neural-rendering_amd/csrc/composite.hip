@@ -24,6 +24,9 @@ namespace anr {
 
 constexpr int kMaxCh = 8;
 
+// 1: always use the generic (LDS-staged) kernels; test hook (anr_composite_force_generic).
+static int g_composite_generic = 0;
+
 template <typename T>
 __device__ __forceinline__ float ldv(const T* p, int64_t i) { return to_f32<T>(p[i]); }
 
@@ -308,7 +311,292 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Register-blocked kernels (SPL = samples per lane known at compile time, C = 4 bands,
+// S in {1, 4}): each lane loads its contiguous block of z / sigma / color ONCE with vector
+// loads into registers; neighbour z values at the block edges come from the adjacent
+// lanes by shuffles. Same math and rounding order per sample as the kernels above.
+namespace rb {
+
+template <typename T>
+__device__ __forceinline__ void load_block(const T* p, int n, float* dst) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) dst[i] = to_f32<T>(p[i]);
+}
+template <>
+__device__ __forceinline__ void load_block<float>(const float* p, int n, float* dst) {
+  if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < n; i += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(p + i);
+      dst[i] = v.x; dst[i + 1] = v.y; dst[i + 2] = v.z; dst[i + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < n; ++i) dst[i] = p[i];
+  }
+}
+
+// delta for the lane's SPL samples (graphics_utils.py:30-34); zs = z * z_scale.
+template <int SPL>
+__device__ __forceinline__ void deltas(const float* zr, float zscale, int i0, int nvalid, int N,
+                                       int lane, float* dl) {
+  float zs[SPL];
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) zs[j] = j < nvalid ? zr[j] * zscale : 0.0f;
+  const float prev = shfl_up(zs[SPL - 1], 1);  // last sample of lane-1
+  const float next = shfl_down(zs[0], 1);      // first sample of lane+1
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) {
+    const int i = i0 + j;
+    const float zi = zs[j];
+    const float zprev = j == 0 ? prev : zs[j - 1];
+    const float znext = j == SPL - 1 ? next : zs[j + 1];
+    const float lo = i == 0 ? zi * 0.0f : (zprev + zi) / 2.0f;
+    const float hi = i == N - 1 ? zi : (zi + znext) / 2.0f;
+    dl[j] = hi - lo;
+  }
+}
+
+template <typename T, int SPL, int S>
+__global__ void __launch_bounds__(256) fwd_kernel(CompArgs a) {
+  constexpr int C = 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
+  if (b >= a.B) return;
+  const int N = a.N;
+  const int i0 = lane * SPL;
+  const int nvalid = max(0, min(SPL, N - i0));
+  const float* zr = a.z + b * N + i0;
+  float dl[SPL], sg[SPL * S], col[SPL * C];
+  deltas<SPL>(zr, a.z_scale, i0, nvalid, N, lane, dl);
+  if (nvalid == SPL) {
+    load_block<T>(static_cast<const T*>(a.sigma) + (b * N + i0) * S, SPL * S, sg);
+    load_block<T>(static_cast<const T*>(a.color) + (b * N + i0) * C, SPL * C, col);
+  } else {
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        sg[j * S + s] = j < nvalid ? ldv(static_cast<const T*>(a.sigma), (b * N + i0 + j) * S + s) : 0.0f;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        col[j * C + c] = j < nvalid ? ldv(static_cast<const T*>(a.color), (b * N + i0 + j) * C + c) : 0.0f;
+    }
+  }
+  float al[SPL * S], pt[S], pom[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) pt[s] = pom[s] = 1.0f;
+#pragma unroll
+  for (int j = 0; j < SPL; ++j)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const float x = 1.0f - expf(-sg[j * S + s] * dl[j]);
+      al[j * S + s] = j < nvalid ? x : 0.0f;
+      pt[s] *= (1.0f - al[j * S + s]) + (j < nvalid ? 1e-10f : 0.0f);
+      pom[s] *= 1.0f - al[j * S + s];
+    }
+  float Tin[S], Stot[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    Tin[s] = wave_excl_prod(pt[s], lane);
+    Stot[s] = wave_prod(pom[s]);
+  }
+  float cm[C] = {0.0f, 0.0f, 0.0f, 0.0f};
+  T* wout = a.weights ? static_cast<T*>(a.weights) + (b * N + i0) * S : nullptr;
+  T* aout = a.alpha ? static_cast<T*>(a.alpha) + (b * N + i0) * S : nullptr;
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) {
+    float w[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      w[s] = al[j * S + s] * Tin[s];
+      Tin[s] *= (1.0f - al[j * S + s]) + 1e-10f;
+      if (j < nvalid) {
+        if (wout) wout[j * S + s] = from_f32<T>(w[s]);
+        if (aout) aout[j * S + s] = from_f32<T>(al[j * S + s]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) cm[c] += col[j * C + c] * w[S == 1 ? 0 : c];
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float atmo = wave_sum(cm[c]);
+    float surf = 0.0f;
+    if (a.color_surf) surf = Stot[S == 1 ? 0 : c] * ldv(static_cast<const T*>(a.color_surf), b * C + c);
+    if (lane == 0) {
+      static_cast<T*>(a.color_map)[b * C + c] = from_f32<T>(atmo + surf);
+      if (a.atmo) static_cast<T*>(a.atmo)[b * C + c] = from_f32<T>(atmo);
+      if (a.surf) static_cast<T*>(a.surf)[b * C + c] = from_f32<T>(surf);
+    }
+  }
+}
+
+template <typename T, int SPL, int S>
+__global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
+  constexpr int C = 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
+  if (b >= a.B) return;  // wave-uniform
+  const int N = a.N;
+  const int i0 = lane * SPL;
+  const int nvalid = max(0, min(SPL, N - i0));
+  const float* zr = a.z + b * N + i0;
+  float dl[SPL], sg[SPL * S], col[SPL * C];
+  deltas<SPL>(zr, a.z_scale, i0, nvalid, N, lane, dl);
+  if (nvalid == SPL) {
+    load_block<T>(static_cast<const T*>(a.sigma) + (b * N + i0) * S, SPL * S, sg);
+    load_block<T>(static_cast<const T*>(a.color) + (b * N + i0) * C, SPL * C, col);
+  } else {
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        sg[j * S + s] = j < nvalid ? ldv(static_cast<const T*>(a.sigma), (b * N + i0 + j) * S + s) : 0.0f;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        col[j * C + c] = j < nvalid ? ldv(static_cast<const T*>(a.color), (b * N + i0 + j) * C + c) : 0.0f;
+    }
+  }
+  float ga[C], gs[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float dc = a.d_color_map ? ldv(static_cast<const T*>(a.d_color_map), b * C + c) : 0.0f;
+    ga[c] = dc + (a.d_atmo ? ldv(static_cast<const T*>(a.d_atmo), b * C + c) : 0.0f);
+    gs[c] = dc + (a.d_surf ? ldv(static_cast<const T*>(a.d_surf), b * C + c) : 0.0f);
+  }
+  // forward over the block: e = exp(-sigma*delta), alpha, local prefixes, lane aggregates
+  float e[SPL * S], al[SPL * S], Tl[SPL * S], Pl[SPL * S], q[SPL * S];
+  float pt[S], pom[S], A[S], Bv[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) { pt[s] = pom[s] = A[s] = 1.0f; Bv[s] = 0.0f; }
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) {
+    float qq[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) qq[s] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) qq[S == 1 ? 0 : c] += col[j * C + c] * ga[c];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int o = j * S + s;
+      if (a.d_weights && j < nvalid) qq[s] += ldv(static_cast<const T*>(a.d_weights), (b * N + i0 + j) * S + s);
+      const float ee = expf(-sg[o] * dl[j]);
+      e[o] = ee;
+      al[o] = j < nvalid ? 1.0f - ee : 0.0f;
+      q[o] = j < nvalid ? qq[s] : 0.0f;
+      const float t = (1.0f - al[o]) + (j < nvalid ? 1e-10f : 0.0f);
+      Tl[o] = pt[s];
+      Pl[o] = pom[s];
+      pt[s] *= t;
+      pom[s] *= 1.0f - al[o];
+      Bv[s] = Bv[s] + A[s] * q[o] * al[o];
+      A[s] = A[s] * t;
+    }
+  }
+  float Tin[S], Pin[S], Q[S], V[S], Stot[S], r[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    Tin[s] = wave_excl_prod(pt[s], lane);
+    Pin[s] = wave_excl_prod(pom[s], lane);
+    Q[s] = wave_excl_suffix_prod(pom[s], lane);
+    Stot[s] = wave_prod(pom[s]);
+    V[s] = wave_affine_suffix(A[s], Bv[s], lane);
+    r[s] = 0.0f;
+  }
+  if (a.color_surf) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      r[S == 1 ? 0 : c] += ldv(static_cast<const T*>(a.color_surf), b * C + c) * gs[c];
+  }
+  float dD[SPL];
+  T* dcol = a.d_color ? static_cast<T*>(a.d_color) + (b * N + i0) * C : nullptr;
+  T* dsig = a.d_sigma ? static_cast<T*>(a.d_sigma) + (b * N + i0) * S : nullptr;
+#pragma unroll
+  for (int j = SPL - 1; j >= 0; --j) {
+    float dd = 0.0f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int o = j * S + s;
+      const float Ti = Tin[s] * Tl[o];
+      const float Pi = Pin[s] * Pl[o];
+      const float w = al[o] * Ti;
+      if (dcol && j < nvalid) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          if (S == 1 || c == s) dcol[j * C + c] = from_f32<T>(w * ga[c]);
+      }
+      float dal = Ti * (q[o] - V[s]) - r[s] * Pi * Q[s];
+      if (a.d_alpha && j < nvalid) dal += ldv(static_cast<const T*>(a.d_alpha), (b * N + i0 + j) * S + s);
+      if (dsig && j < nvalid) dsig[j * S + s] = from_f32<T>(dal * e[o] * dl[j]);
+      dd += dal * e[o] * sg[o];
+      const float t = (1.0f - al[o]) + (j < nvalid ? 1e-10f : 0.0f);
+      V[s] = q[o] * al[o] + t * V[s];
+      Q[s] *= 1.0f - al[o];
+    }
+    dD[j] = j < nvalid ? dd : 0.0f;
+  }
+  if (a.d_color_surf && lane == 0) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      static_cast<T*>(a.d_color_surf)[b * C + c] = from_f32<T>(Stot[S == 1 ? 0 : c] * gs[c]);
+  }
+  if (a.d_z) {
+    const float dprev = shfl_up(dD[SPL - 1], 1);
+    const float dnext = shfl_down(dD[0], 1);
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+      const int i = i0 + j;
+      if (j >= nvalid) break;
+      const float dm1 = j == 0 ? dprev : dD[j - 1];
+      const float dp1 = j == SPL - 1 ? dnext : dD[j + 1];
+      float g = 0.0f;
+      if (i >= 1) g += 0.5f * (dm1 - dD[j]);
+      if (i + 1 <= N - 1) g += 0.5f * (dD[j] - dp1);
+      if (i == N - 1) g += dD[j];
+      a.d_z[b * N + i] = g * a.z_scale;
+    }
+  }
+}
+
+}  // namespace rb
+
+// Launch a register-blocked kernel if (C, S, N) is covered; returns false otherwise.
+template <typename T>
+static bool launch_rb(bool bwd, const CompArgs& a, hipStream_t st) {
+  if (a.C != 4 || !(a.S == 1 || a.S == 4)) return false;
+  const int spl = (a.N + 63) / 64;
+  const dim3 grid(static_cast<unsigned>(ceil_div(a.B, 4))), block(256);
+#define ANR_RB(SPL, S)                                                              \
+  do {                                                                              \
+    if (bwd)                                                                        \
+      hipLaunchKernelGGL((rb::bwd_kernel<T, SPL, S>), grid, block, 0, st, a);       \
+    else                                                                            \
+      hipLaunchKernelGGL((rb::fwd_kernel<T, SPL, S>), grid, block, 0, st, a);       \
+  } while (0)
+#define ANR_RB_S(SPL) \
+  if (a.S == 1) ANR_RB(SPL, 1); else ANR_RB(SPL, 4); return true;
+  switch (spl) {
+    case 1: ANR_RB_S(1)
+    case 2: ANR_RB_S(2)
+    case 3: ANR_RB_S(3)
+    case 4: ANR_RB_S(4)
+    case 8: ANR_RB_S(8)
+    case 16: ANR_RB_S(16)
+    default: return false;
+  }
+#undef ANR_RB_S
+#undef ANR_RB
+}
 }  // namespace anr
+
+extern "C" int anr_composite_force_generic(int32_t on) {
+  const int prev = anr::g_composite_generic;
+  anr::g_composite_generic = on ? 1 : 0;
+  return prev;
+}
 
 extern "C" int anr_composite_fwd(const float* z, float z_scale, const void* color,
                                  const void* sigma, const void* color_surf, int32_t io_dtype,
@@ -327,6 +615,12 @@ extern "C" int anr_composite_fwd(const float* z, float z_scale, const void* colo
   a.B = B; a.N = N; a.C = C; a.S = S;
   a.color_map = color_map; a.atmo = color_map_atmo; a.surf = color_map_surf;
   a.weights = weights; a.alpha = alpha;
+  if (!g_composite_generic &&
+      (io_dtype == ANR_F16 ? launch_rb<__half>(false, a, as_stream(stream))
+                           : launch_rb<float>(false, a, as_stream(stream)))) {
+    ANR_CHECK_LAUNCH("anr_composite_fwd(rb)");
+    return ANR_OK;
+  }
   const dim3 grid(static_cast<unsigned>(ceil_div(B, 4))), block(256);
   if (io_dtype == ANR_F16)
     hipLaunchKernelGGL(composite_fwd_kernel<__half>, grid, block, 0, as_stream(stream), a);
@@ -358,6 +652,12 @@ extern "C" int anr_composite_bwd(const float* z, float z_scale, const void* colo
   a.d_color_map = d_color_map; a.d_atmo = d_atmo; a.d_surf = d_surf;
   a.d_weights = d_weights; a.d_alpha = d_alpha;
   a.d_color = d_color; a.d_sigma = d_sigma; a.d_color_surf = d_color_surf; a.d_z = d_z;
+  if (!g_composite_generic &&
+      (io_dtype == ANR_F16 ? launch_rb<__half>(true, a, as_stream(stream))
+                           : launch_rb<float>(true, a, as_stream(stream)))) {
+    ANR_CHECK_LAUNCH("anr_composite_bwd(rb)");
+    return ANR_OK;
+  }
   const size_t per_wave = static_cast<size_t>(2 * S + 1) * N * sizeof(float);
   int waves = 4;
   while (waves > 1 && waves * per_wave > 64 * 1024) --waves;

@@ -23,6 +23,7 @@
 #include "anr_common.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace anr {
 
@@ -248,6 +249,216 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_kernel(
   if (have) flush();
 }
 
+
+// ---------------------------------------------------------------------------------------
+// v2 (F = 2, L <= 16): 4 lanes per level, one chunk of K consecutive samples per wave.
+// lane = 4*level + 2*b + f owns feature f of the 2^(D-1) corners whose x-offset is b.
+// The 4 lanes of a level touch entries (x, x+1) x features (0, 1): adjacent addresses on
+// dense levels (and on hashed levels when x is even, since the first hash prime is 1),
+// so one wave instruction issues one memory request per level instead of four. When
+// the sample moves to a neighbouring cell with the same x, corners shared by the two
+// cells keep their accumulated gradient (bwd) / gathered feature (fwd).
+template <int D>
+struct Corners {
+  static constexpr int NC = 1 << (D - 1);
+  // lattice offset bit of corner c (0..NC-1) along dim d >= 1
+  __device__ static int bit(int c, int d) { return (c >> (d - 1)) & 1; }
+};
+
+// Map the per-lane corners of the old cell onto the new cell (same x): returns, for each
+// old corner, the new corner index or -1 if it leaves the new cell.
+template <int D>
+__device__ __forceinline__ void corner_shift(const uint32_t* oldc, const uint32_t* newc,
+                                             bool same_x, int* map) {
+#pragma unroll
+  for (int c = 0; c < Corners<D>::NC; ++c) {
+    bool keep = same_x;
+    int nc = 0;
+#pragma unroll
+    for (int d = 1; d < D; ++d) {
+      const int nb = static_cast<int>(oldc[d] + Corners<D>::bit(c, d)) - static_cast<int>(newc[d]);
+      keep = keep && (nb == 0 || nb == 1);
+      nc |= (nb & 1) << (d - 1);
+    }
+    map[c] = keep ? nc : -1;
+  }
+}
+
+template <int D>
+__device__ __forceinline__ uint32_t corner_index(const uint32_t* cell, int b, int c,
+                                                 uint32_t T, uint32_t res) {
+  uint32_t gc[D];
+  gc[0] = cell[0] + b;
+#pragma unroll
+  for (int d = 1; d < D; ++d) gc[d] = cell[d] + Corners<D>::bit(c, d);
+  return grid_index<D>(T, res, gc);
+}
+
+template <int D, typename TT, typename TO>
+__global__ void __launch_bounds__(256) hashgrid_fwd_v2_kernel(
+    GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
+    int64_t K, const TT* __restrict__ table, TO* __restrict__ out, int64_t out_stride) {
+  constexpr int NC = Corners<D>::NC;
+  const int lane = threadIdx.x & 63;
+  const int level = lane >> 2, b = (lane >> 1) & 1, f = lane & 1;
+  const int64_t chunk = __builtin_amdgcn_readfirstlane(
+      static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6));
+  const int64_t m0 = chunk * K;
+  if (m0 >= M) return;  // wave-uniform
+  const int64_t m1 = m0 + K < M ? m0 + K : M;
+  const bool active = level < n_levels;
+  const int lv = active ? level : 0;
+  const float scale = G.scale[lv];
+  const uint32_t res = G.res[lv];
+  const uint32_t T = G.size[lv];
+  const TT* __restrict__ grid = table + static_cast<int64_t>(G.offset[lv]) * 2 + f;
+
+  uint32_t cell[D];
+  bool have = false;
+#pragma unroll
+  for (int d = 0; d < D; ++d) cell[d] = 0u;
+  float val[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) val[c] = 0.0f;
+
+  for (int64_t m = m0; m < m1; ++m) {
+    float w[D];
+    uint32_t g[D];
+    bool same = have;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float p = fmaf(scale, x[m * x_stride + d], 0.5f);
+      const float fl = floorf(p);
+      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
+      w[d] = p - fl;
+      same = same && (g[d] == cell[d]);
+    }
+    if (active && !same) {
+      int map[NC];
+      corner_shift<D>(cell, g, have && g[0] == cell[0], map);
+      float nval[NC];
+      bool got[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        nval[c] = 0.0f;
+        got[c] = false;
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int c2 = 0; c2 < NC; ++c2)
+          if (map[c] == c2) {
+            nval[c2] = val[c];
+            got[c2] = true;
+          }
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (!got[c]) nval[c] = to_f32<TT>(grid[static_cast<int64_t>(corner_index<D>(g, b, c, T, res)) * 2]);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) val[c] = nval[c];
+#pragma unroll
+      for (int d = 0; d < D; ++d) cell[d] = g[d];
+      have = true;
+    }
+    // partial sum over this lane's corners, in tcnn's weight order (x, then y, z)
+    const float wx = b ? w[0] : 1.0f - w[0];
+    float part = 0.0f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float wt = wx;
+#pragma unroll
+      for (int d = 1; d < D; ++d) wt *= Corners<D>::bit(c, d) ? w[d] : 1.0f - w[d];
+      part = fmaf(wt, val[c], part);
+    }
+    // add the partner lane (other x-offset): lane ^ 2 within the quad (DPP quad_perm 2,3,0,1)
+    const float other = __int_as_float(__builtin_amdgcn_update_dpp(
+        0, __float_as_int(part), 0x4E, 0xF, 0xF, false));
+    const float tot = b ? other + part : part + other;
+    if (active && b == 0) out[m * out_stride + level * 2 + f] = from_f32<TO>(tot);
+  }
+}
+
+template <int D, typename TG>
+__global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
+    GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
+    int64_t K, const TG* __restrict__ dout, int64_t dout_stride, float* __restrict__ dtable) {
+  constexpr int NC = Corners<D>::NC;
+  const int lane = threadIdx.x & 63;
+  const int level = lane >> 2, b = (lane >> 1) & 1, f = lane & 1;
+  const int64_t chunk = __builtin_amdgcn_readfirstlane(
+      static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6));
+  const int64_t m0 = chunk * K;
+  if (m0 >= M || level >= n_levels) return;
+  const int64_t m1 = m0 + K < M ? m0 + K : M;
+  const float scale = G.scale[level];
+  const uint32_t res = G.res[level];
+  const uint32_t T = G.size[level];
+  float* __restrict__ grad = dtable + static_cast<int64_t>(G.offset[level]) * 2 + f;
+
+  uint32_t cell[D];
+  bool have = false;
+#pragma unroll
+  for (int d = 0; d < D; ++d) cell[d] = 0u;
+  float acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = 0.0f;
+
+  for (int64_t m = m0; m < m1; ++m) {
+    float w[D];
+    uint32_t g[D];
+    bool same = have;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float p = fmaf(scale, x[m * x_stride + d], 0.5f);
+      const float fl = floorf(p);
+      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
+      w[d] = p - fl;
+      same = same && (g[d] == cell[d]);
+    }
+    if (!same) {
+      if (have) {
+        int map[NC];
+        corner_shift<D>(cell, g, g[0] == cell[0], map);
+        float nacc[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) nacc[c] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (map[c] < 0) {
+            if (acc[c] != 0.0f)
+              atomicAdd(grad + static_cast<int64_t>(corner_index<D>(cell, b, c, T, res)) * 2,
+                        acc[c]);
+          } else {
+#pragma unroll
+            for (int c2 = 0; c2 < NC; ++c2)
+              if (map[c] == c2) nacc[c2] = acc[c];
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] = nacc[c];
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) cell[d] = g[d];
+      have = true;
+    }
+    const float gv = to_f32<TG>(dout[m * dout_stride + level * 2 + f]);
+    const float wx = b ? w[0] : 1.0f - w[0];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float wt = wx;
+#pragma unroll
+      for (int d = 1; d < D; ++d) wt *= Corners<D>::bit(c, d) ? w[d] : 1.0f - w[d];
+      acc[c] = fmaf(wt, gv, acc[c]);
+    }
+  }
+  if (have) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (acc[c] != 0.0f)
+        atomicAdd(grad + static_cast<int64_t>(corner_index<D>(cell, b, c, T, res)) * 2, acc[c]);
+  }
+}
+
 static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
   if (d->n_levels < 1 || d->n_levels > ANR_MAX_LEVELS) return false;
   for (int l = 0; l < d->n_levels; ++l) {
@@ -259,6 +470,24 @@ static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
   }
   return true;
 }
+
+// v2: one chunk per wave; aim for >= 32K waves (8 per SIMD on 1024 SIMDs, x4 slack).
+static int64_t pick_chunk_v2(int64_t M) {
+  int64_t K = M / 32768;
+  if (K < 1) K = 1;
+  if (K > 128) K = 128;
+  return K;
+}
+
+// Kernel generation per direction. Mode 0 (default): forward v1, backward v2 (measured
+// fastest on the ray-coherent bench workload); 1: both v1; 2: both v2.
+// ANR_HASHGRID_MODE or anr_hashgrid_force_v1() selects it (test hook).
+static int g_hashgrid_mode = [] {
+  const char* e = getenv("ANR_HASHGRID_MODE");
+  return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
+}();
+static bool fwd_v2() { return g_hashgrid_mode == 2; }
+static bool bwd_v2() { return g_hashgrid_mode != 1; }
 
 // Samples per chunk: long chunks amortise the per-cell gathers/atomics, but the grid
 // must still fill 256 CUs. Aim for >= 64K chunks.
@@ -273,6 +502,22 @@ template <int D, int F>
 static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const float* x,
                       int64_t x_stride, int64_t M, const void* table, int32_t tdt,
                       void* out, int32_t odt, int64_t out_stride, hipStream_t s) {
+  if (F == 2 && d->n_levels <= 16 && fwd_v2()) {
+    const int64_t K = pick_chunk_v2(M);
+    const int64_t waves = ceil_div(M, K);
+    const dim3 grid(static_cast<unsigned>(ceil_div(waves, 4))), block(256);
+#define ANR_HG_FWD2(TT, TO)                                                                  \
+  hipLaunchKernelGGL((hashgrid_fwd_v2_kernel<D, TT, TO>), grid, block, 0, s, G, d->n_levels, \
+                     x, x_stride, M, K, static_cast<const TT*>(table), static_cast<TO*>(out), \
+                     out_stride)
+    if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD2(__half, __half);
+    else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD2(__half, float);
+    else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD2(float, __half);
+    else ANR_HG_FWD2(float, float);
+#undef ANR_HG_FWD2
+    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v2)");
+    return ANR_OK;
+  }
   const int lpc = d->n_levels <= 16 ? 16 : 32;
   const int64_t K = pick_chunk(M);
   const int64_t chunks = ceil_div(M, K);
@@ -295,6 +540,21 @@ template <int D, int F>
 static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const float* x,
                       int64_t x_stride, int64_t M, const void* dout, int32_t gdt,
                       int64_t dout_stride, float* dtable, hipStream_t s) {
+  if (F == 2 && d->n_levels <= 16 && bwd_v2()) {
+    const int64_t K = pick_chunk_v2(M);
+    const int64_t waves = ceil_div(M, K);
+    const dim3 grid(static_cast<unsigned>(ceil_div(waves, 4))), block(256);
+    if (gdt == ANR_F16)
+      hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<D, __half>), grid, block, 0, s, G,
+                         d->n_levels, x, x_stride, M, K, static_cast<const __half*>(dout),
+                         dout_stride, dtable);
+    else
+      hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<D, float>), grid, block, 0, s, G,
+                         d->n_levels, x, x_stride, M, K, static_cast<const float*>(dout),
+                         dout_stride, dtable);
+    ANR_CHECK_LAUNCH("anr_hashgrid_bwd(v2)");
+    return ANR_OK;
+  }
   const int lpc = d->n_levels <= 16 ? 16 : 32;
   const int64_t K = pick_chunk(M);
   const int64_t chunks = ceil_div(M, K);
@@ -313,6 +573,12 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 }
 
 }  // namespace anr
+
+extern "C" int anr_hashgrid_force_v1(int32_t mode) {
+  const int prev = anr::g_hashgrid_mode;
+  anr::g_hashgrid_mode = (mode >= 0 && mode <= 2) ? mode : 0;
+  return prev;
+}
 
 extern "C" int anr_hashgrid_init(anr_hashgrid_desc* d, int32_t n_dims, int32_t n_levels,
                                  int32_t n_features, int32_t base_resolution,

@@ -15,8 +15,9 @@
 // * dW accumulates in registers (f32) across every row tile a wavefront processes and
 //   is flushed once per wavefront with coalesced f32 atomics (16 lanes = 64 contiguous
 //   bytes). The generic kernel instead did one LDS atomic per dW element per tile.
-// * f16 gradients are scaled per 16-row tile by a power of two (max |g| -> 256) and
-//   unscaled exactly when folded into the f32 dW registers.
+// * f16 gradients are scaled by one power of two per wavefront (max |dL/dout| over the
+//   wave's rows -> 256, found by a pre-pass over dout) and unscaled exactly in f32 when
+//   dW is flushed and when dL/din is written.
 
 #include "anr_common.h"
 
@@ -313,9 +314,40 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
   for (int t = 0; t < S::n_tiles; ++t) dw[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
   const int64_t n_tiles = (a.M + 15) / 16;
+  // f16: one power-of-two gradient scale per wavefront (max |dL/dout| over all its rows
+  // -> 256), so dW accumulates directly in the MFMA accumulators and is unscaled once.
+  float s = 1.0f, inv_s = 1.0f;
+  if constexpr (half) {
+    float gmax = 0.0f;
+    for (int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave; tile < n_tiles;
+         tile += static_cast<int64_t>(gridDim.x) * waves) {
+      for (int e = lane; e < 16 * a.n_out; e += 64) {
+        const int r = e / a.n_out, c = e - r * a.n_out;
+        const int64_t row = tile * 16 + r;
+        if (row < a.M) gmax = fmaxf(gmax, fabsf(load_dyn(a.dout, a.dout_dt, row * a.dout_stride + c)));
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) gmax = fmaxf(gmax, shfl_xor(gmax, m));
+    if (gmax > 0.0f) {
+      int e2 = static_cast<int>(floorf(log2f(256.0f / gmax)));
+      e2 = e2 < -60 ? -60 : (e2 > 100 ? 100 : e2);
+      s = ldexpf(1.0f, e2);
+      inv_s = ldexpf(1.0f, -e2);
+    }
+  }
+  TC* const w_base = w;
+  TC* const wt_base = wt;
   for (int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave; tile < n_tiles;
        tile += static_cast<int64_t>(gridDim.x) * waves) {
     const int64_t r0 = tile * 16;
+    // Re-read weight fragments from LDS every tile instead of letting the compiler hoist
+    // them into ~110 VGPRs: with the register-resident dW that would cap the kernel at one
+    // wavefront per SIMD. An opaque zero offset keeps the LDS base (ds_read addressing).
+    int zoff = 0;
+    asm volatile("" : "+v"(zoff));
+    w = w_base + zoff;
+    wt = wt_base + zoff;
     // ---- recompute the forward, keeping each layer's input tile
     load_input<TC, S>(a, r0, base + S::acts(0), lane);
     wave_sync();
@@ -344,7 +376,6 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
     }
     // ---- output gradient tile g = dL/d(pre-activation output), scaled for f16
     float gv[NOP / 4];
-    float gmax = 0.0f;
     {
       const int r = lane & 15;
       const int64_t row = r0 + r;
@@ -356,18 +387,6 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
         if (row < a.M && c < a.n_out) v = load_dyn(a.dout, a.dout_dt, row * a.dout_stride + c);
         if (a.out_relu && !(static_cast<float>(outb[r * S::ldo + c]) > 0.0f)) v = 0.0f;
         gv[j] = v;
-        gmax = fmaxf(gmax, fabsf(v));
-      }
-    }
-    float s = 1.0f, inv_s = 1.0f;
-    if constexpr (half) {
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) gmax = fmaxf(gmax, shfl_xor(gmax, m));
-      if (gmax > 0.0f) {
-        int e2 = static_cast<int>(floorf(log2f(256.0f / gmax)));
-        e2 = e2 < -60 ? -60 : (e2 > 100 ? 100 : e2);
-        s = ldexpf(1.0f, e2);
-        inv_s = ldexpf(1.0f, -e2);
       }
     }
 #pragma unroll
@@ -389,14 +408,11 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
       for (int mt = 0; mt < N / 16; ++mt) {
 #pragma unroll
         for (int nt = 0; nt < K / 16; ++nt) {
-          f4 t = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int ks = 0; ks < 16; ks += O::KS)
-            t = O::mma(O::cols(g + ks * S::ldg + mt * 16, S::ldg, lane),
-                       O::cols(act + ks * lda + nt * 16, lda, lane), t);
           f4& d = dw[S::tile_off(k) + mt * (K / 16) + nt];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) d[i] = fmaf(t[i], inv_s, d[i]);
+          for (int ks = 0; ks < 16; ks += O::KS)
+            d = O::mma(O::cols(g + ks * S::ldg + mt * 16, S::ldg, lane),
+                       O::cols(act + ks * lda + nt * 16, lda, lane), d);
         }
       }
       // dAct_k^T (K x 16) = W_kᵀ · gᵀ
@@ -446,7 +462,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = mt * 16 + 4 * (lane >> 4) + i, col = nt * 16 + (lane & 15);
-          if (d[i] != 0.0f) atomicAdd(a.dparams + S::woff(k) + row * K + col, d[i]);
+          if (d[i] != 0.0f) atomicAdd(a.dparams + S::woff(k) + row * K + col, d[i] * inv_s);
         }
       }
   }
@@ -469,9 +485,19 @@ static int launch(bool bwd, const Args& a, hipStream_t st) {
   if (lds > 160 * 1024) return 1;  // does not fit: caller falls back to the generic kernel
   const int64_t tiles = (a.M + 15) / 16;
   int64_t blocks = (tiles + waves - 1) / waves;
-  const int64_t cap = bwd ? 512 : 2048;  // bwd: few waves, each folds many tiles into dW
-  if (blocks > cap) blocks = cap;
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  // bwd: one resident wave per slot, each folding many tiles into its register dW (so
+  // the flush atomics stay few); size the grid to what is co-resident (once per kernel)
+  static int per_cu[2] = {0, 0};
+  int& pc = per_cu[bwd ? 1 : 0];
+  if (pc == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * waves, lds) != hipSuccess || nb < 1)
+      nb = 1;
+    pc = nb;
+  }
+  const int64_t cap = bwd ? 256LL * pc : 2048;
+  if (blocks > cap) blocks = cap;
   if (bwd)
     hipLaunchKernelGGL((bwd_kernel<TC, W, NIP, NOP, NH>), dim3(blocks), dim3(64 * waves), lds,
                        st, a);

@@ -111,6 +111,11 @@ int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x, int64_t x_strid
                      int64_t M, const void* table, int32_t table_dtype, void* out,
                      int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
 
+/* Kernel generation: 0 = default (forward v1 one-lane-per-level, backward v2
+ * four-lanes-per-level), 1 = v1 both, 2 = v2 both. Test hook; process-wide. Returns the
+ * previous mode. */
+int anr_hashgrid_force_v1(int32_t mode);
+
 /* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)
  * f32, ACCUMULATED (caller zeroes). Duplicate corner updates inside a wavefront are
  * pre-summed before the f32 atomics (samples along one ray share cells). */
@@ -185,6 +190,9 @@ int anr_composite_fwd(const float* z, float z_scale, const void* color, const vo
                       int32_t C, int32_t S, void* color_map, void* color_map_atmo,
                       void* color_map_surf, void* weights, void* alpha,
                       anr_stream_t stream);
+/* Use the generic kernels instead of the register-blocked ones (C = 4, S in {1,4},
+ * N/64 in {1,2,3,4,8,16}). Test hook; process-wide. Returns the previous setting. */
+int anr_composite_force_generic(int32_t on);
 /* Backward. Gradients in (nullable; io_dtype): d_color_map, d_atmo, d_surf (B,C),
  * d_weights (B,N,S), d_alpha (B,N,S). Outputs (nullable): d_color (B,N,C),
  * d_sigma (B,N,S), d_color_surf (B,C) (io_dtype), d_z (B,N) f32 (dL/dz before scaling

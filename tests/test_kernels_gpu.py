@@ -109,12 +109,24 @@ def _grid_inputs(dev, cfg, M, coherent, seed=0):
     return x.contiguous()
 
 
+@pytest.fixture(params=["v2", "v1"])
+def hash_path(request):
+    from atmonr_amd import _lib
+
+    prev = _lib.load().anr_hashgrid_force_v1(1 if request.param == "v1" else 2)
+    yield request.param
+    _lib.load().anr_hashgrid_force_v1(prev)
+
+
 @pytest.mark.parametrize("cfg,M,coherent", [((3, 16, 16, 1.3819, 19), 5000, False),
                                             ((3, 16, 16, 1.3819, 19), 8192, True),
                                             ((3, 16, 16, 1.3819, 21), 3001, True),
                                             ((2, 16, 16, 1.3819, 19), 4096, False),
-                                            ((3, 6, 4, 2.0, 10), 777, True)])
-def test_hashgrid_fwd_bwd_f32(dev, cfg, M, coherent):
+                                            ((3, 6, 4, 2.0, 10), 777, True),
+                                            ((3, 16, 16, 1.3819, 19), 300000, True),
+                                            ((2, 16, 16, 1.3819, 19), 70000, True),
+                                            ((3, 20, 16, 1.3, 15), 2000, True)])
+def test_hashgrid_fwd_bwd_f32(dev, hash_path, cfg, M, coherent):
     from atmonr_amd import _lib
 
     d = _lib.hashgrid_desc(cfg[0], cfg[1], 2, cfg[2], cfg[3], cfg[4])
@@ -137,7 +149,7 @@ def test_hashgrid_fwd_bwd_f32(dev, cfg, M, coherent):
     close(dtab, gref, rel=1e-5, atol=1e-5)
 
 
-def test_hashgrid_f16_table_and_strided_output(dev):
+def test_hashgrid_f16_table_and_strided_output(dev, hash_path):
     from atmonr_amd import _lib
 
     cfg = (3, 16, 16, 1.3819, 19)
@@ -253,8 +265,17 @@ def test_mlp_fwd_bwd(dev, mlp_path, n_in, n_out, width, n_hidden, out_relu, half
 
 
 # ------------------------------------------------------------------ K8
+@pytest.fixture(params=["blocked", "generic"])
+def comp_path(request):
+    from atmonr_amd import _lib
+
+    prev = _lib.load().anr_composite_force_generic(1 if request.param == "generic" else 0)
+    yield request.param
+    _lib.load().anr_composite_force_generic(prev)
+
+
 @pytest.mark.parametrize("tag", ["f32", "f32long", "f32multi", "f16"])
-def test_composite_vs_reference(dev, tag):
+def test_composite_vs_reference(dev, comp_path, tag):
     from atmonr_amd.graphics_utils import render, render_with_surface
 
     g = golden("render.npz")
@@ -280,7 +301,7 @@ def test_composite_vs_reference(dev, tag):
     close(cm2.float(), torch.from_numpy(g[f"{tag}_plain_cm"]), rel=rel, atol=atol)
 
 
-def test_composite_known_answers(dev):
+def test_composite_known_answers(dev, comp_path):
     from atmonr_amd.graphics_utils import render_with_surface
 
     B, N = 3, 100

@@ -105,13 +105,9 @@ def main():
 
     # one flat f32 gradient bucket; every param's .grad is a view into it, so backward
     # accumulates in place and DP needs exactly one all-reduce per step
-    params = [p for g in opt.param_groups for p in g["params"]]
-    n_total = sum(p.numel() for p in params)
-    flat = torch.zeros(n_total, device=dev)
-    off = 0
-    for p in params:
-        p.grad = flat[off:off + p.numel()].view_as(p)
-        off += p.numel()
+    from atmonr_amd.parallel import FlatGradBucket
+
+    bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev)
 
     loader = BatchLoader(ds, args.batch, shuffle=True, rank=rank, world_size=world, seed=0)
     it = iter(loader)
@@ -128,10 +124,9 @@ def main():
         batch = next_batch()
         res = pipe.forward(batch)
         loss = pipe.compute_loss(batch, res)
-        flat.zero_()
+        bucket.zero()
         loss.backward()
-        if world > 1:
-            dist.all_reduce(flat, op=dist.ReduceOp.AVG)
+        bucket.all_reduce()
         opt.step()
         return loss
 
@@ -196,7 +191,9 @@ def main():
                 try:
                     data = json.load(open(pmc))
                     key = f"{dominant}:{args.variant}:{args.batch}x{args.samples}"
-                    roofline["traffic"] = data.get(key)
+                    ent = data.get(key)
+                    if ent:  # HBM bytes per launch from rocprofv3 PMC (tools/prof.sh)
+                        roofline["traffic"] = ent["bytes"]
                 except (OSError, ValueError):
                     pass
 

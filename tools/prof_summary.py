@@ -1,0 +1,84 @@
+"""Summarise a tools/prof.sh run into profiles/.
+
+    python tools/prof_summary.py gpurun_out/prof_v3 r01
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, copied), profiles/<tag>_summary.md
+(per-kernel average duration and HBM traffic per launch) and updates
+profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+
+HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes: rocprofv3 reports
+both in KiB; on gfx950 FETCH_SIZE counts exactly half the bytes of wide coalesced reads
+(MI355X_MICROARCH.md §HBM), hence the factor 2. That correction is calibrated for
+streaming reads; for the gather-heavy hash kernels it is an upper-bound estimate.
+"""
+
+from __future__ import annotations
+
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# bench.py kernel tag -> substring of the mangled/demangled kernel name
+TAGS = {
+    "hash_fwd": "hashgrid_fwd_kernel<3, 2, __half, __half>",
+    "hash_bwd": "hashgrid_bwd_v2_kernel<3, float>",
+    "dir_mlp_bwd": "bwd_kernelIDF16_Li64ELi32ELi16ELi2E",
+    "pos_mlp_bwd": "bwd_kernelIDF16_Li64ELi32ELi16ELi1E",
+    "dir_mlp_fwd": "fwd_kernelIDF16_Li64ELi32ELi16ELi2E",
+    "pos_mlp_fwd": "fwd_kernelIDF16_Li64ELi32ELi16ELi1E",
+    "composite_fwd": "rb::fwd_kernel<float, 16, 1>",
+    "composite_bwd": "rb::bwd_kernel<float, 16, 1>",
+    "sampler": "sample_uniform_bins_kernel",
+}
+
+
+def per_launch(path: str) -> dict[str, float]:
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main(src: str, tag: str, key_suffix: str = "baseline:8192x1024"):
+    prof = os.path.join(ROOT, "profiles")
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    fetch = per_launch(os.path.join(src, "fetch", "run_counter_collection.csv"))
+    write = per_launch(os.path.join(src, "write", "run_counter_collection.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    pmc_path = os.path.join(prof, "pmc_traffic.json")
+    pmc = json.load(open(pmc_path)) if os.path.exists(pmc_path) else {}
+    lines = [f"# rocprofv3 summary ({tag})", "",
+             "bench.py (config-3 train step, 8192 rays x 1024 samples), "
+             "`rocprofv3 --kernel-trace --stats` plus separate `--pmc FETCH_SIZE` and "
+             "`--pmc WRITE_SIZE` passes (tools/prof.sh). Traffic = (2*FETCH_SIZE + "
+             "WRITE_SIZE) KiB per launch (gfx950 FETCH_SIZE half-count correction).", "",
+             "| kernel | calls | avg us | % time | HBM traffic / launch (MB) |",
+             "|---|---|---|---|---|"]
+    for r in rows[:25]:
+        name = r["Name"]
+        f = next((v for k, v in fetch.items() if k == name or k.startswith(name[:80])), None)
+        w = next((v for k, v in write.items() if k == name or k.startswith(name[:80])), None)
+        traffic = (2 * f + w) * 1024 / 1e6 if f is not None and w is not None else None
+        short = name.replace("|", "/")[:90]
+        lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                     f"{float(r['Percentage']):.1f} | "
+                     f"{'' if traffic is None else f'{traffic:.1f}'} |")
+    for t, pat in TAGS.items():
+        f = next((v for k, v in fetch.items() if pat in k), None)
+        w = next((v for k, v in write.items() if pat in k), None)
+        if f is not None and w is not None:
+            pmc[f"{t}:{key_suffix}"] = {"bytes": round((2 * f + w) * 1024),
+                                        "fetch_kib": round(f, 1), "write_kib": round(w, 1)}
+    json.dump(pmc, open(pmc_path, "w"), indent=1, sort_keys=True)
+    open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

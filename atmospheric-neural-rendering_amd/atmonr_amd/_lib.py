@@ -138,6 +138,31 @@ _SIGNATURES = {
             c_int64, _P, c_int32, c_int64, _P, _P,
         ],
     ),
+    "anr_ingp_dir_mlp_fwd": (
+        c_int32,
+        [POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64, _P, c_int32,
+         c_int64, _P],
+    ),
+    "anr_ingp_dir_mlp_bwd": (
+        c_int32,
+        [POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64, _P, c_int64, _P,
+         _P, c_int64, _P, _P],
+    ),
+    "anr_ingp_field_supported": (c_int32, [POINTER(MlpDesc), POINTER(MlpDesc)]),
+    "anr_ingp_field_packed_size": (c_int64, [POINTER(MlpDesc), POINTER(MlpDesc)]),
+    "anr_ingp_field_set_grad_scale": (c_int32, [c_int32]),
+    "anr_ingp_field_pack": (
+        c_int32, [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, _P, _P]),
+    "anr_ingp_field_fwd": (
+        c_int32,
+        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
+         c_int64, _P],
+    ),
+    "anr_ingp_field_bwd": (
+        c_int32,
+        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
+         c_int64, _P, c_int64, _P, _P, _P],
+    ),
     "anr_composite_force_generic": (c_int32, [c_int32]),
     "anr_composite_fwd": (
         c_int32,

@@ -5,14 +5,23 @@ One autograd node for the per-sample part of InstantNGPPipeline.forward
 
     pos_enc = pos_encoder(pts)                          K3   (f16 table, f16 features)
     pos_out = pos_mlp(pos_enc)                          K6   (f16 MFMA, f32 out)
-    dir_enc = dir_encoder(cat[dirs, pos_out[:, 1:]])    K5   (SH deg 2 | identity)
-    color   = relu(dir_mlp(dir_enc))                    K6   (output ReLU in-kernel)
-    sigma   = relu(pos_out[:, 0])
+    dir_enc = dir_encoder(cat[dirs, pos_out[:, 1:]])    \\
+    color   = relu(dir_mlp(dir_enc))                    /  K6 with the dir encoding fused
+    sigma   = relu(pos_out[:, 0])                          into its input loader
 
 Inside the node the hash tables and MLP weights use the modules' compute dtype (f16 by
-default, as tcnn) but every activation gradient crosses kernel boundaries in f32, so
-none of the gradient chain underflows f16 (the reference's fp16-end-to-end autograd,
-survey §0, loses small gradients; the f16 MLP backward here rescales per tile).
+default, as tcnn) while every activation gradient crosses kernel boundaries in f32, so
+the gradient chain does not underflow f16 (the reference's fp16 autograd does; survey
+§0). The backward is three kernels: the dir-MLP backward writes dL/dpos_out directly
+(density ReLU included), the pos-MLP backward writes dL/denc, the hash backward scatters
+into the table gradient. When a parameter already has a float32 ``.grad`` (e.g. a
+FlatGradBucket view), the kernels accumulate into it directly and the node returns no
+gradient for that parameter — the same result as autograd's accumulation, one pass less.
+
+With f16 networks of the shapes both reference configs use (pos 32->W->16, dir 19->W(x1|2)
+->nb, W in {32, 64}) the two MLPs and the dir encoding run as ONE kernel each way
+(anr_ingp_field_fwd/bwd): pos_out and dL/dpos_out stay in registers, the backward writes
+only dL/denc. The weights are packed into MFMA fragment order once per forward.
 """
 
 from __future__ import annotations
@@ -25,6 +34,13 @@ from . import _lib
 from ._lib import call, dtype_code, ptr
 
 
+def _grad_target(param: torch.nn.Parameter, dev) -> tuple[torch.Tensor, bool]:
+    g = param.grad
+    if g is not None and g.dtype == torch.float32 and g.is_contiguous() and g.device == dev:
+        return g, True
+    return torch.zeros(param.shape, device=dev, dtype=torch.float32), False
+
+
 class IngpFieldFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, coords, dirs, n_per_ray: int, p_hash, p_pos, p_dir, pipe):
@@ -32,70 +48,75 @@ class IngpFieldFn(torch.autograd.Function):
         dev = coords.device
         s = _lib.stream(dev)
         M = coords.shape[0]
-        enc_mod, pos_mod, dir_mod = pipe.pos_encoder, pipe.pos_mlp, pipe.dir_encoder
-        dmlp = pipe.dir_mlp
+        enc_mod, pos_mod = pipe.pos_encoder, pipe.pos_mlp
         grid = enc_mod.hash_grids[0]
         cdt = pos_mod.dtype
         prec = _lib.F16 if cdt == torch.float16 else _lib.F32
         t_hash = p_hash.detach().to(enc_mod.dtype)
-        w_pos = p_pos.detach().to(cdt)
-        w_dir = p_dir.detach().to(cdt)
+        dirs = dirs.float().contiguous()
 
         enc = torch.empty(M, grid.n_out, device=dev, dtype=enc_mod.dtype)
         call("anr_hashgrid_fwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(t_hash),
              dtype_code(t_hash.dtype), ptr(enc), dtype_code(enc.dtype), enc.stride(0), s,
              tag="hash_fwd")
+        ctx.pipe = pipe
+        ctx.n_per_ray = n_per_ray
+        ctx.params = (p_hash, p_pos, p_dir)
+        if field_fused(pipe) and enc.dtype == torch.float16:
+            pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
+            packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc),
+                                 device=dev, dtype=torch.float16)
+            m_pos, m_dir = p_pos.detach().float(), p_dir.detach().float()  # f32 masters
+            call("anr_ingp_field_pack", pdesc, ddesc, ptr(m_pos), ptr(m_dir), ptr(packed), s,
+                 tag="field_pack")
+            sigma = torch.empty(M, device=dev, dtype=torch.float32)
+            color = torch.empty(M, pipe.dir_mlp.n_output_dims, device=dev, dtype=torch.float32)
+            call("anr_ingp_field_fwd", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
+                 ptr(dirs), n_per_ray, M, ptr(sigma), ptr(color), color.stride(0), s,
+                 tag="field_fwd")
+            ctx.fused_field = True
+            ctx.save_for_backward(coords, dirs, enc, packed)
+            return sigma, color
+        ctx.fused_field = False
+        w_pos = p_pos.detach().to(cdt)
+        w_dir = p_dir.detach().to(cdt)
         pos_out = torch.empty(M, pos_mod.n_output_dims, device=dev, dtype=torch.float32)
         call("anr_mlp_fwd", ctypes.byref(pos_mod.desc), prec, ptr(w_pos), ptr(enc),
              dtype_code(enc.dtype), enc.stride(0), M, ptr(pos_out), _lib.F32,
              pos_out.stride(0), s, tag="pos_mlp_fwd")
-        # dir encoding input: [SH(dir) | pos_out[:, 1:]]  (19 columns, tcnn pads to 32)
-        n_sh = dir_mod.n_output_dims - (pos_mod.n_output_dims - 1)
-        dir_in = torch.empty(M, dir_mod.n_output_dims, device=dev, dtype=cdt)
-        dirs_rep = dirs.float().repeat_interleave(n_per_ray, dim=0)
-        sh_leaf = dir_mod._leaves[0][1]
-        call("anr_sh_fwd", sh_leaf.degree, ptr(dirs_rep), 3, M, ptr(dir_in), dtype_code(cdt),
-             dir_in.stride(0), s)
-        call("anr_identity", pos_out.data_ptr() + 4, _lib.F32, pos_out.stride(0), M,
-             pos_mod.n_output_dims - 1, dir_in.data_ptr() + n_sh * dir_in.element_size(),
-             dtype_code(cdt), dir_in.stride(0), s)
-        color = torch.empty(M, dmlp.n_output_dims, device=dev, dtype=torch.float32)
-        call("anr_mlp_fwd", ctypes.byref(pipe._dir_desc_relu), prec, ptr(w_dir), ptr(dir_in),
-             dtype_code(cdt), dir_in.stride(0), M, ptr(color), _lib.F32, color.stride(0), s,
-             tag="dir_mlp_fwd")
+        color = torch.empty(M, pipe.dir_mlp.n_output_dims, device=dev, dtype=torch.float32)
+        call("anr_ingp_dir_mlp_fwd", ctypes.byref(pipe._dir_desc_relu), prec, ptr(w_dir),
+             ptr(pos_out), pos_out.stride(0), ptr(dirs), n_per_ray, M, ptr(color), _lib.F32,
+             color.stride(0), s, tag="dir_mlp_fwd")
         sigma = torch.relu(pos_out[:, 0])
-        ctx.save_for_backward(coords, enc, pos_out, dir_in, t_hash, w_pos, w_dir)
-        ctx.pipe = pipe
-        ctx.n_sh = n_sh
+        ctx.save_for_backward(coords, dirs, enc, pos_out, w_pos, w_dir)
         return sigma, color
 
     @staticmethod
     def backward(ctx, d_sigma, d_color):
-        coords, enc, pos_out, dir_in, t_hash, w_pos, w_dir = ctx.saved_tensors
+        if ctx.fused_field:
+            return IngpFieldFn._backward_fused(ctx, d_sigma, d_color)
+        coords, dirs, enc, pos_out, w_pos, w_dir = ctx.saved_tensors
         pipe = ctx.pipe
         dev = coords.device
         s = _lib.stream(dev)
         M = coords.shape[0]
-        pos_mod, dmlp, enc_mod = pipe.pos_mlp, pipe.dir_mlp, pipe.pos_encoder
+        pos_mod, enc_mod = pipe.pos_mlp, pipe.pos_encoder
         grid = enc_mod.hash_grids[0]
         prec = _lib.F16 if pos_mod.dtype == torch.float16 else _lib.F32
-        g_dir = torch.zeros(dmlp.params.shape, device=dev, dtype=torch.float32)
-        g_pos = torch.zeros(pos_mod.params.shape, device=dev, dtype=torch.float32)
-        g_hash = torch.zeros(enc_mod.params.shape, device=dev, dtype=torch.float32)
+        p_hash, p_pos, p_dir = ctx.params
+        g_hash, direct_h = _grad_target(p_hash, dev)
+        g_pos, direct_p = _grad_target(p_pos, dev)
+        g_dir, direct_d = _grad_target(p_dir, dev)
         if d_color is None:
-            d_color = torch.zeros(M, dmlp.n_output_dims, device=dev)
+            d_color = torch.zeros(M, pipe.dir_mlp.n_output_dims, device=dev)
         d_color = d_color.float().contiguous()
-        d_dir_in = torch.empty(M, dir_in.shape[1], device=dev, dtype=torch.float32)
-        call("anr_mlp_bwd", ctypes.byref(pipe._dir_desc_relu), prec, ptr(w_dir), ptr(dir_in),
-             dtype_code(dir_in.dtype), dir_in.stride(0), M, ptr(d_color), _lib.F32,
-             d_color.stride(0), ptr(d_dir_in), _lib.F32, d_dir_in.stride(0), ptr(g_dir), s,
-             tag="dir_mlp_bwd")
+        d_sigma = d_sigma.float().contiguous() if d_sigma is not None else None
         d_pos_out = torch.empty_like(pos_out)
-        d_pos_out[:, 1:] = d_dir_in[:, ctx.n_sh:]
-        if d_sigma is None:
-            d_pos_out[:, 0] = 0
-        else:
-            d_pos_out[:, 0] = d_sigma.float() * (pos_out[:, 0] > 0)
+        call("anr_ingp_dir_mlp_bwd", ctypes.byref(pipe._dir_desc_relu), prec, ptr(w_dir),
+             ptr(pos_out), pos_out.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(d_color),
+             d_color.stride(0), ptr(d_sigma), ptr(d_pos_out), d_pos_out.stride(0), ptr(g_dir),
+             s, tag="dir_mlp_bwd")
         d_enc = torch.empty(M, enc.shape[1], device=dev, dtype=torch.float32)
         call("anr_mlp_bwd", ctypes.byref(pos_mod.desc), prec, ptr(w_pos), ptr(enc),
              dtype_code(enc.dtype), enc.stride(0), M, ptr(d_pos_out), _lib.F32,
@@ -103,4 +124,44 @@ class IngpFieldFn(torch.autograd.Function):
              tag="pos_mlp_bwd")
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
-        return None, None, None, g_hash, g_pos, g_dir, None
+        return (None, None, None, None if direct_h else g_hash, None if direct_p else g_pos,
+                None if direct_d else g_dir, None)
+
+    @staticmethod
+    def _backward_fused(ctx, d_sigma, d_color):
+        coords, dirs, enc, packed = ctx.saved_tensors
+        pipe = ctx.pipe
+        dev = coords.device
+        s = _lib.stream(dev)
+        M = coords.shape[0]
+        grid = pipe.pos_encoder.hash_grids[0]
+        p_hash, p_pos, p_dir = ctx.params
+        g_hash, direct_h = _grad_target(p_hash, dev)
+        g_pos, direct_p = _grad_target(p_pos, dev)
+        g_dir, direct_d = _grad_target(p_dir, dev)
+        if d_color is None:
+            d_color = torch.zeros(M, pipe.dir_mlp.n_output_dims, device=dev)
+        d_color = d_color.float().contiguous()
+        d_sigma = d_sigma.float().contiguous() if d_sigma is not None else None
+        d_enc = torch.empty(M, enc.shape[1], device=dev, dtype=torch.float32)
+        pdesc, ddesc = ctypes.byref(pipe.pos_mlp.desc), ctypes.byref(pipe.dir_mlp.desc)
+        call("anr_ingp_field_bwd", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
+             ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color), d_color.stride(0),
+             ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), s, tag="field_bwd")
+        call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
+             _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
+        return (None, None, None, None if direct_h else g_hash, None if direct_p else g_pos,
+                None if direct_d else g_dir, None)
+
+
+def field_fused(pipe) -> bool:
+    """True when the pipeline's networks run through anr_ingp_field_{fwd,bwd}."""
+    flag = getattr(pipe, "_field_fused", None)
+    if flag is None:
+        ok = (pipe.pos_mlp.dtype == torch.float16 and pipe.dir_mlp.dtype == torch.float16
+              and getattr(pipe, "allow_field_fusion", True))
+        if ok:
+            ok = bool(_lib.load().anr_ingp_field_supported(ctypes.byref(pipe.pos_mlp.desc),
+                                                           ctypes.byref(pipe.dir_mlp.desc)))
+        pipe._field_fused = flag = ok
+    return flag

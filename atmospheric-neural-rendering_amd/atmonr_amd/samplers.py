@@ -50,13 +50,15 @@ def sample_uniform_bins(
     device = origin.device
     if u is None:
         u = _uniform(B, n_bins, device, random)
+    if u is not None:  # bound to a name: a temporary's block could be reused by _bins()
+        u = u.float().contiguous()
     origin = origin.float().contiguous()
     direction = direction.float().contiguous()
     length = length.float().contiguous()
     pts = torch.empty(B, n_bins, 3, device=device)
     z = torch.empty(B, n_bins, device=device)
     call("anr_sample_uniform_bins", ptr(origin), ptr(direction), ptr(length),
-         ptr(u.contiguous()) if u is not None else None, ptr(_bins(n_bins, device)), B, n_bins,
+         ptr(u), ptr(_bins(n_bins, device)), B, n_bins,
          ptr(pts), ptr(z), None, None, _lib.stream(device))
     return pts, z
 
@@ -78,6 +80,8 @@ def sample_and_preprocess(
     device = origin.device
     if u is None:
         u = _uniform(B, n_bins, device, random)
+    if u is not None:  # bound to a name: a temporary's block could be reused by _bins()
+        u = u.float().contiguous()
     origin = origin.float().contiguous()
     direction = direction.float().contiguous()
     length = length.float().contiguous()
@@ -85,7 +89,7 @@ def sample_and_preprocess(
     z = torch.empty(B, n_bins, device=device)
     coords = torch.empty(B, n_bins, 3, device=device)
     call("anr_sample_uniform_bins", ptr(origin), ptr(direction), ptr(length),
-         ptr(u.contiguous()) if u is not None else None, ptr(_bins(n_bins, device)), B, n_bins,
+         ptr(u), ptr(_bins(n_bins, device)), B, n_bins,
          ptr(pts), ptr(z), prep, ptr(coords), _lib.stream(device))
     return pts, z, coords
 

@@ -109,6 +109,14 @@ struct Args {
   int out_dt;
   int64_t out_stride;
   float* dparams;
+  // MODE 1 (Instant-NGP dir MLP, instant_ngp.py:165-171): the input row is
+  // [SH2(dir of its ray) | pos_out[r, 1:16] | 1.0 ...] built on the fly; the backward
+  // writes dL/dpos_out (col 0 = dL/dsigma * [pos_out[r,0] > 0], cols 1.. from dIn).
+  const float* pos_out;
+  int64_t pos_stride;
+  const float* dirs;
+  int64_t n_per_ray;
+  const float* d_sigma;
 };
 
 // Compile-time network shape.
@@ -177,11 +185,65 @@ __device__ void stage_weights(const Args& a, TC* w, TC* wt) {
   }
 }
 
+// SH degree 2 of a direction remapped from [0,1] coordinates (tcnn convention: the raw
+// direction is fed as if in [0,1], i.e. 2d-1; instant_ngp.py:165-169).
+__device__ __forceinline__ float sh2(int c, float x, float y, float z) {
+  x = x * 2.0f - 1.0f;
+  y = y * 2.0f - 1.0f;
+  z = z * 2.0f - 1.0f;
+  return c == 0 ? 0.28209479177387814f
+                : (c == 1 ? -0.48860251190291987f * y
+                          : (c == 2 ? 0.48860251190291987f * z : -0.48860251190291987f * x));
+}
+
 // Load a 16-row input tile into act0 (ld = lda(0)); pad columns with 1.0.
-template <typename TC, typename S>
+template <typename TC, typename S, int MODE>
 __device__ void load_input(const Args& a, int64_t r0, TC* act0, int lane) {
   constexpr int NIP = S::K(0);
   constexpr int ld = S::lda(0);
+  if constexpr (MODE == 1) {
+    // [SH2(dir) (4) | pos_out[:, 1:16] (15) | 1.0 (13)], NIP == 32: lane = (row, 8-column
+    // part); one 32-bit division per row, pos_out read as float4s.
+    static_assert(NIP == 32, "dir mode expects 19 inputs padded to 32");
+    const int r = lane & 15, part = lane >> 4;
+    const int64_t row = r0 + r;
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.0f;
+    if (row < a.M) {
+      const float* po = a.pos_out + row * a.pos_stride;
+      if (part == 0) {
+        const uint32_t ray = static_cast<uint32_t>(row) / static_cast<uint32_t>(a.n_per_ray);
+        const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
+        const float x = d[0] * 2.0f - 1.0f, y = d[1] * 2.0f - 1.0f, z = d[2] * 2.0f - 1.0f;
+        v[0] = 0.28209479177387814f;
+        v[1] = -0.48860251190291987f * y;
+        v[2] = 0.48860251190291987f * z;
+        v[3] = -0.48860251190291987f * x;
+        const float4 p1 = *reinterpret_cast<const float4*>(po);      // cols 0..3
+        const float4 p2 = *reinterpret_cast<const float4*>(po + 4);  // cols 4..7
+        v[4] = p1.y; v[5] = p1.z; v[6] = p1.w; v[7] = p2.x;
+      } else if (part == 1) {
+        const float4 p2 = *reinterpret_cast<const float4*>(po + 4);
+        const float4 p3 = *reinterpret_cast<const float4*>(po + 8);
+        const float4 p4 = *reinterpret_cast<const float4*>(po + 12);
+        v[0] = p2.y; v[1] = p2.z; v[2] = p2.w; v[3] = p3.x;
+        v[4] = p3.y; v[5] = p3.z; v[6] = p3.w; v[7] = p4.x;
+      } else if (part == 2) {
+        const float4 p4 = *reinterpret_cast<const float4*>(po + 12);
+        v[0] = p4.y; v[1] = p4.z; v[2] = p4.w;
+#pragma unroll
+        for (int i = 3; i < 8; ++i) v[i] = 1.0f;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 1.0f;
+      }
+    }
+    TC* dst = act0 + r * ld + part * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dst[i] = static_cast<TC>(v[i]);
+    return;
+  }
   if constexpr (sizeof(TC) == 2) {
     if (a.in_dt == ANR_F16 && a.n_in == NIP && (a.in_stride % 8) == 0) {
       // 16 rows x NIP halves, 16 bytes per lane per chunk
@@ -226,7 +288,7 @@ __device__ __forceinline__ void hidden_layer(const TC* w, const TC* src, TC* dst
   }
 }
 
-template <typename TC, int W, int NIP, int NOP, int NH>
+template <typename TC, int W, int NIP, int NOP, int NH, int MODE>
 __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   using S = Shape<W, NIP, NOP, NH>;
   using O = Ops<TC>;
@@ -244,7 +306,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   for (int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave; tile < n_tiles;
        tile += static_cast<int64_t>(gridDim.x) * waves) {
     const int64_t r0 = tile * 16;
-    load_input<TC, S>(a, r0, act0, lane);
+    load_input<TC, S, MODE>(a, r0, act0, lane);
     wave_sync();
     hidden_layer<TC, S, 0>(w, act0, hA, W + 8, lane);
     wave_sync();
@@ -291,7 +353,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   }
 }
 
-template <typename TC, int W, int NIP, int NOP, int NH>
+template <typename TC, int W, int NIP, int NOP, int NH, int MODE>
 __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
   using S = Shape<W, NIP, NOP, NH>;
   using O = Ops<TC>;
@@ -349,7 +411,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
     w = w_base + zoff;
     wt = wt_base + zoff;
     // ---- recompute the forward, keeping each layer's input tile
-    load_input<TC, S>(a, r0, base + S::acts(0), lane);
+    load_input<TC, S, MODE>(a, r0, base + S::acts(0), lane);
     wave_sync();
     hidden_layer<TC, S, 0>(w, base + S::acts(0), base + S::acts(1), S::lda(1), lane);
     wave_sync();
@@ -429,6 +491,23 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) acc[i] = av[i] > 0.0f ? acc[i] : 0.0f;
             O::store_t(gn + nt * 16, S::ldg, acc, lane);
+          } else if constexpr (MODE == 1) {
+            // dIn columns 4..18 are dL/dpos_out[:, 1..15]; column 0 of dL/dpos_out is
+            // dL/dsigma through the density ReLU (instant_ngp.py:178,184).
+            const int64_t row = r0 + (lane & 15);
+            const int c0 = nt * 16 + 4 * (lane >> 4);
+            if (row < a.M) {
+              float* dp = static_cast<float*>(a.out) + row * a.out_stride;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int c = c0 + i;
+                if (c >= 4 && c < 19) dp[c - 3] = acc[i] * inv_s;
+              }
+              if (c0 == 0) {
+                const float ds = a.d_sigma ? a.d_sigma[row] : 0.0f;
+                dp[0] = a.pos_out[row * a.pos_stride] > 0.0f ? ds : 0.0f;
+              }
+            }
           } else {
             const int64_t row = r0 + (lane & 15);
             const int c0 = nt * 16 + 4 * (lane >> 4);
@@ -468,7 +547,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
   }
 }
 
-template <typename TC, int W, int NIP, int NOP, int NH>
+template <typename TC, int W, int NIP, int NOP, int NH, int MODE>
 static int launch(bool bwd, const Args& a, hipStream_t st) {
   using S = Shape<W, NIP, NOP, NH>;
   const size_t es = sizeof(TC);
@@ -477,10 +556,10 @@ static int launch(bool bwd, const Args& a, hipStream_t st) {
   const void* fn;
   if (bwd) {
     lds = (static_cast<size_t>(S::w_lds) + S::wt_lds + waves * S::wave_bwd) * es;
-    fn = reinterpret_cast<const void*>(&bwd_kernel<TC, W, NIP, NOP, NH>);
+    fn = reinterpret_cast<const void*>(&bwd_kernel<TC, W, NIP, NOP, NH, MODE>);
   } else {
     lds = (static_cast<size_t>(S::w_lds) + waves * S::wave_fwd) * es;
-    fn = reinterpret_cast<const void*>(&fwd_kernel<TC, W, NIP, NOP, NH>);
+    fn = reinterpret_cast<const void*>(&fwd_kernel<TC, W, NIP, NOP, NH, MODE>);
   }
   if (lds > 160 * 1024) return 1;  // does not fit: caller falls back to the generic kernel
   const int64_t tiles = (a.M + 15) / 16;
@@ -499,11 +578,11 @@ static int launch(bool bwd, const Args& a, hipStream_t st) {
   const int64_t cap = bwd ? 256LL * pc : 2048;
   if (blocks > cap) blocks = cap;
   if (bwd)
-    hipLaunchKernelGGL((bwd_kernel<TC, W, NIP, NOP, NH>), dim3(blocks), dim3(64 * waves), lds,
-                       st, a);
+    hipLaunchKernelGGL((bwd_kernel<TC, W, NIP, NOP, NH, MODE>), dim3(blocks), dim3(64 * waves),
+                       lds, st, a);
   else
-    hipLaunchKernelGGL((fwd_kernel<TC, W, NIP, NOP, NH>), dim3(blocks), dim3(64 * waves), lds,
-                       st, a);
+    hipLaunchKernelGGL((fwd_kernel<TC, W, NIP, NOP, NH, MODE>), dim3(blocks), dim3(64 * waves),
+                       lds, st, a);
   return 0;
 }
 
@@ -513,7 +592,7 @@ static int dispatch_tc(const anr_mlp_desc* d, bool bwd, const Args& a, hipStream
   const int key = d->width * 10000 + d->n_input_padded * 10 + d->n_hidden_layers;
   switch (key) {
 #define ANR_CASE(W, NIP, NH) \
-  case W * 10000 + NIP * 10 + NH: return launch<TC, W, NIP, 16, NH>(bwd, a, st);
+  case W * 10000 + NIP * 10 + NH: return launch<TC, W, NIP, 16, NH, 0>(bwd, a, st);
     ANR_CASE(32, 16, 1) ANR_CASE(32, 32, 1) ANR_CASE(32, 48, 1)
     ANR_CASE(32, 16, 2) ANR_CASE(32, 32, 2) ANR_CASE(32, 48, 2)
     ANR_CASE(64, 16, 1) ANR_CASE(64, 32, 1) ANR_CASE(64, 48, 1)
@@ -521,6 +600,16 @@ static int dispatch_tc(const anr_mlp_desc* d, bool bwd, const Args& a, hipStream
 #undef ANR_CASE
     default: return 1;
   }
+}
+
+template <typename TC>
+static int dispatch_dir(const anr_mlp_desc* d, bool bwd, const Args& a, hipStream_t st) {
+  if (d->n_output_padded != 16 || d->n_input != 19 || d->n_input_padded != 32) return 1;
+  if (d->width == 64 && d->n_hidden_layers == 2) return launch<TC, 64, 32, 16, 2, 1>(bwd, a, st);
+  if (d->width == 32 && d->n_hidden_layers == 2) return launch<TC, 32, 32, 16, 2, 1>(bwd, a, st);
+  if (d->width == 64 && d->n_hidden_layers == 1) return launch<TC, 64, 32, 16, 1, 1>(bwd, a, st);
+  if (d->width == 32 && d->n_hidden_layers == 1) return launch<TC, 32, 32, 16, 1, 1>(bwd, a, st);
+  return 1;
 }
 
 }  // namespace fused
@@ -552,3 +641,85 @@ int mlp_fused_try(const anr_mlp_desc* d, int32_t precision, bool bwd, const void
 }
 
 }  // namespace anr
+
+// ---------------------------------------------------------------------------------------
+// Instant-NGP dir MLP with the dir encoding fused into its input (instant_ngp.py:165-171).
+extern "C" int anr_ingp_dir_mlp_fwd(const anr_mlp_desc* d, int32_t precision,
+                                    const void* params, const float* pos_out,
+                                    int64_t pos_stride, const float* dirs, int64_t n_per_ray,
+                                    int64_t M, void* color, int32_t out_dtype,
+                                    int64_t out_stride, anr_stream_t stream) {
+  using namespace anr;
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(d && params && pos_out && dirs && color, "anr_ingp_dir_mlp_fwd: null argument");
+  ANR_CHECK_ARG(precision == ANR_F16 || precision == ANR_F32, "anr_ingp_dir_mlp_fwd: precision");
+  ANR_CHECK_ARG(n_per_ray >= 1 && pos_stride >= 16 && pos_stride % 4 == 0 &&
+                    out_stride >= d->n_output && M < (1LL << 31),
+                "anr_ingp_dir_mlp_fwd: bad shape/stride");
+  fused::Args a{};
+  a.n_in = d->n_input;
+  a.n_out = d->n_output;
+  a.out_relu = d->output_activation == ANR_ACT_RELU;
+  a.M = M;
+  a.params = params;
+  a.out = color;
+  a.out_dt = out_dtype;
+  a.out_stride = out_stride;
+  a.pos_out = pos_out;
+  a.pos_stride = pos_stride;
+  a.dirs = dirs;
+  a.n_per_ray = n_per_ray;
+  const int rc = precision == ANR_F16 ? fused::dispatch_dir<_Float16>(d, false, a, as_stream(stream))
+                                      : fused::dispatch_dir<float>(d, false, a, as_stream(stream));
+  if (rc != 0) {
+    set_error("anr_ingp_dir_mlp_fwd: unsupported network shape (width %d, hidden %d, in %d)",
+              d->width, d->n_hidden_layers, d->n_input);
+    return ANR_E_UNSUPPORTED;
+  }
+  ANR_CHECK_LAUNCH("anr_ingp_dir_mlp_fwd");
+  return ANR_OK;
+}
+
+extern "C" int anr_ingp_dir_mlp_bwd(const anr_mlp_desc* d, int32_t precision,
+                                    const void* params, const float* pos_out,
+                                    int64_t pos_stride, const float* dirs, int64_t n_per_ray,
+                                    int64_t M, const float* d_color, int64_t d_color_stride,
+                                    const float* d_sigma, float* d_pos_out,
+                                    int64_t d_pos_stride, float* dparams,
+                                    anr_stream_t stream) {
+  using namespace anr;
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(d && params && pos_out && dirs && d_color && d_pos_out && dparams,
+                "anr_ingp_dir_mlp_bwd: null argument");
+  ANR_CHECK_ARG(precision == ANR_F16 || precision == ANR_F32, "anr_ingp_dir_mlp_bwd: precision");
+  ANR_CHECK_ARG(n_per_ray >= 1 && pos_stride >= 16 && pos_stride % 4 == 0 &&
+                    d_pos_stride >= 16 && d_color_stride >= d->n_output && M < (1LL << 31),
+                "anr_ingp_dir_mlp_bwd: bad shape/stride");
+  fused::Args a{};
+  a.n_in = d->n_input;
+  a.n_out = d->n_output;
+  a.out_relu = d->output_activation == ANR_ACT_RELU;
+  a.M = M;
+  a.params = params;
+  a.dout = d_color;
+  a.dout_dt = ANR_F32;
+  a.dout_stride = d_color_stride;
+  a.out = d_pos_out;
+  a.out_dt = ANR_F32;
+  a.out_stride = d_pos_stride;
+  a.dparams = dparams;
+  a.pos_out = pos_out;
+  a.pos_stride = pos_stride;
+  a.dirs = dirs;
+  a.n_per_ray = n_per_ray;
+  a.d_sigma = d_sigma;
+  const int rc = precision == ANR_F16 ? fused::dispatch_dir<_Float16>(d, true, a, as_stream(stream))
+                                      : fused::dispatch_dir<float>(d, true, a, as_stream(stream));
+  if (rc != 0) {
+    set_error("anr_ingp_dir_mlp_bwd: unsupported network shape (width %d, hidden %d, in %d)",
+              d->width, d->n_hidden_layers, d->n_input);
+    return ANR_E_UNSUPPORTED;
+  }
+  ANR_CHECK_LAUNCH("anr_ingp_dir_mlp_bwd");
+  return ANR_OK;
+}

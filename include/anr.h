@@ -176,6 +176,56 @@ int anr_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void* params,
                 int32_t din_dtype, int64_t din_stride, float* dparams,
                 anr_stream_t stream);
 
+/* Instant-NGP dir MLP with the dir encoding fused into its input
+ * (instant_ngp.py:165-171): row r of the network input is
+ * [SH degree 2 of dirs[r / n_per_ray] | pos_out[r, 1:16] | 1.0 padding] (n_input = 19,
+ * padded 32), so the encoded tensor is never materialised.
+ *   pos_out (M, >=16) f32 (pos_mlp output, row stride pos_stride); dirs (M/n_per_ray, 3)
+ *   f32; color (M, n_output) out_dtype. Widths 32/64, 1-2 hidden layers. */
+int anr_ingp_dir_mlp_fwd(const anr_mlp_desc* d, int32_t precision, const void* params,
+                         const float* pos_out, int64_t pos_stride, const float* dirs,
+                         int64_t n_per_ray, int64_t M, void* color, int32_t out_dtype,
+                         int64_t out_stride, anr_stream_t stream);
+/* Backward: d_color (M, n_output) f32, d_sigma (M,) f32 (nullable) -> d_pos_out (M, 16)
+ * f32 WRITTEN: column 0 = d_sigma * [pos_out[:,0] > 0] (density ReLU, instant_ngp.py:184),
+ * columns 1..15 = dL/d(pos_out[:, 1:16]); dparams f32 ACCUMULATED. */
+int anr_ingp_dir_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void* params,
+                         const float* pos_out, int64_t pos_stride, const float* dirs,
+                         int64_t n_per_ray, int64_t M, const float* d_color,
+                         int64_t d_color_stride, const float* d_sigma, float* d_pos_out,
+                         int64_t d_pos_stride, float* dparams, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * K6 + K7 fused: the Instant-NGP radiance field after the hash encoding, one kernel each
+ * way (replaces pos_mlp -> dir_encoder -> dir_mlp -> relu at instant_ngp.py:163-184).
+ * ------------------------------------------------------------------------------------
+ * Supported pairs: pos 32 -> W -> 16 (1 hidden layer, no output activation), dir 19 -> W
+ * (1 or 2 hidden layers) -> n_output <= 16, W in {32, 64}; f16 compute only.
+ * Weights: anr_ingp_field_pack converts the f32 master parameters of both networks
+ * (tcnn layout) into one f16 buffer of anr_ingp_field_packed_size halves (MFMA fragment
+ * order); run it after every optimizer step.
+ * Forward: enc (M, >=32) f16 (16-byte aligned rows), dirs (M/n_per_ray, 3) f32 ->
+ *   sigma (M,) f32 = relu(pos_out[:,0]), color (M, n_output) f32 = relu(dir_mlp(...)).
+ * Backward: d_sigma (M,) f32 (nullable), d_color (M, n_output) f32 -> d_enc (M, 32) f32
+ *   WRITTEN; g_pos / g_dir f32 parameter gradients ACCUMULATED. */
+int anr_ingp_field_supported(const anr_mlp_desc* pos, const anr_mlp_desc* dir);
+int64_t anr_ingp_field_packed_size(const anr_mlp_desc* pos, const anr_mlp_desc* dir);
+/* f16 gradient scale target of the backward (max |dL/dout| per wavefront -> 2^v);
+ * returns the previous value. Test hook; process-wide. */
+int anr_ingp_field_set_grad_scale(int32_t log2_target);
+int anr_ingp_field_pack(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                        const float* pos_params, const float* dir_params, void* packed,
+                        anr_stream_t stream);
+int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const void* packed,
+                       const void* enc, int64_t enc_stride, const float* dirs,
+                       int64_t n_per_ray, int64_t M, float* sigma, float* color,
+                       int64_t color_stride, anr_stream_t stream);
+int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const void* packed,
+                       const void* enc, int64_t enc_stride, const float* dirs,
+                       int64_t n_per_ray, int64_t M, const float* d_sigma,
+                       const float* d_color, int64_t d_color_stride, float* d_enc,
+                       int64_t d_enc_stride, float* g_pos, float* g_dir, anr_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * K8: transmittance / alpha-composite integrator, render + render_with_surface
  * (graphics_utils.py:6-77), one wavefront per ray with shuffle prefix scans.

@@ -160,7 +160,8 @@ def test_hashgrid_f16_table_and_strided_output(dev, hash_path):
     x = _grid_inputs(dev, cfg, M, True, seed=3)
     big = torch.full((M, 40), -7.0, device=dev, dtype=torch.float16)  # write cols 4..35
     xd = x.to(dev)
-    _lib.call("anr_hashgrid_fwd", ctypes.byref(d), xd.data_ptr(), 3, M, table.to(dev).data_ptr(),
+    table_d = table.to(dev)  # keep the device copy alive across the launch
+    _lib.call("anr_hashgrid_fwd", ctypes.byref(d), xd.data_ptr(), 3, M, table_d.data_ptr(),
               _lib.F16, big.data_ptr() + 4 * 2, _lib.F16, 40, _lib.stream(dev))
     ref = ref_tcnn.hashgrid_fwd(x.numpy(), table.float().numpy(), cfg)
     close(big[:, 4:36].float(), ref, rel=2e-3, atol=1e-5)
@@ -183,7 +184,8 @@ def test_sh_fwd_bwd(dev, degree):
     close(out, ref_tcnn.sh(x.numpy(), degree), rel=1e-6, atol=1e-6)
     dout = torch.randn(M, degree * degree, generator=gen)
     dx = torch.zeros(M, 3, device=dev)
-    _lib.call("anr_sh_bwd", degree, xd.data_ptr(), 3, M, dout.to(dev).data_ptr(), _lib.F32,
+    dout_d = dout.to(dev)
+    _lib.call("anr_sh_bwd", degree, xd.data_ptr(), 3, M, dout_d.data_ptr(), _lib.F32,
               degree * degree, dx.data_ptr(), 3, s)
     xx = x.double().requires_grad_(True)
     sh = torch.from_numpy(ref_tcnn.sh(x.numpy(), degree))  # value check only
@@ -372,3 +374,168 @@ def test_adam_matches_torch(dev, decoupled, wd):
         ob.step()
     close(pa.detach(), pb.detach(), rel=1e-5, atol=1e-6)
     close(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"], rel=1e-5, atol=1e-12)
+
+
+# ------------------------------------------------------------------ fused dir encoding + MLP
+@pytest.mark.parametrize("width,half", [(64, True), (64, False), (32, True)])
+def test_ingp_dir_mlp_matches_unfused(dev, width, half):
+    """anr_ingp_dir_mlp_{fwd,bwd} == SH2(dir) | pos_out[:,1:] -> padded MLP (oracle)."""
+    from atmonr_amd import _lib
+
+    gen = torch.Generator().manual_seed(width)
+    n_per_ray, R = 37, 29
+    M = n_per_ray * R
+    d = _lib.mlp_desc(19, 4, width, 2, True)
+    nparam = _lib.load().anr_mlp_n_params(ctypes.byref(d))
+    params = torch.randn(nparam, generator=gen) * (1.0 / width) ** 0.5
+    pos_out = torch.randn(M, 16, generator=gen)
+    dirs = torch.nn.functional.normalize(torch.randn(R, 3, generator=gen), dim=1)
+    sh = torch.from_numpy(ref_tcnn.sh(dirs.repeat_interleave(n_per_ray, 0).numpy(), 2))
+    # re-draw rows whose hidden pre-activations sit on a ReLU kink (|h| < 1e-4): there an
+    # f32 kernel and the f64 reference legitimately disagree on the mask (seed 64 has a
+    # row at 2e-8)
+    w_in = params[: width * 32].double().view(width, 32)
+    w_h = params[width * 32: width * 32 + width * width].double().view(width, width)
+    for _ in range(20):
+        x0 = torch.cat([sh, pos_out[:, 1:].double(), torch.ones(M, 13, dtype=torch.float64)], 1)
+        h0 = x0 @ w_in.T
+        h1 = torch.relu(h0) @ w_h.T
+        tied = (torch.minimum(h0.abs().min(1).values, h1.abs().min(1).values) < 1e-4)
+        if not tied.any():
+            break
+        pos_out[tied] = torch.randn(int(tied.sum()), 16, generator=gen)
+    assert not tied.any()
+    dt = torch.float16 if half else torch.float32
+    prec = _lib.F16 if half else _lib.F32
+    s = _lib.stream(dev)
+    pd, pod, dd = params.to(dev).to(dt), pos_out.to(dev), dirs.to(dev)
+    color = torch.empty(M, 4, device=dev)
+    _lib.call("anr_ingp_dir_mlp_fwd", ctypes.byref(d), prec, pd.data_ptr(), pod.data_ptr(), 16,
+              dd.data_ptr(), n_per_ray, M, color.data_ptr(), _lib.F32, 4, s)
+    por = pos_out.double().requires_grad_(True)
+    x = torch.cat([sh, por[:, 1:]], dim=1)
+    pr = params.double().requires_grad_(True)
+    ref = ref_tcnn.mlp_fwd(x, pr, 19, 4, width, 2, output_relu=True, half=half)
+    rel = 1e-2 if half else 1e-4
+    close(color, ref.detach(), rel=rel, atol=1e-6)
+    dcol = torch.randn(M, 4, generator=gen) * 1e-2
+    dsig = torch.randn(M, generator=gen) * 1e-2
+    sig = torch.relu(por[:, 0])
+    (ref * dcol.double()).sum().backward(retain_graph=True)
+    (sig * dsig.double()).sum().backward()
+    dpos = torch.empty(M, 16, device=dev)
+    dparams = torch.zeros(nparam, device=dev)
+    # device copies bound to names: a temporary's block would be reused by the next .to()
+    dcol_d, dsig_d = dcol.to(dev), dsig.to(dev)
+    _lib.call("anr_ingp_dir_mlp_bwd", ctypes.byref(d), prec, pd.data_ptr(), pod.data_ptr(), 16,
+              dd.data_ptr(), n_per_ray, M, dcol_d.data_ptr(), 4, dsig_d.data_ptr(),
+              dpos.data_ptr(), 16, dparams.data_ptr(), s)
+    close(dpos, por.grad, rel=rel * 2, atol=1e-8)
+    close(dparams, pr.grad, rel=rel * 2, atol=1e-8)
+
+
+def _field_ref(enc, dirs, n_per_ray, pp, pd, width, nhd, nb):
+    """sigma, color of instant_ngp.py:163-184 in float64 with the f16 kernel's roundings."""
+    pos_out = ref_tcnn.mlp_fwd(enc, pp, 32, 16, width, 1, half=True)
+    sh = torch.from_numpy(ref_tcnn.sh(dirs.detach().repeat_interleave(n_per_ray, 0).numpy(), 2))
+    x = torch.cat([sh, pos_out[:, 1:]], dim=1)
+    color = ref_tcnn.mlp_fwd(x, pd, 19, nb, width, nhd, output_relu=True, half=True)
+    return torch.relu(pos_out[:, 0]), color, pos_out, x
+
+
+def _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd):
+    """min |pre-activation| per row over every ReLU of the field (tie detector)."""
+    h = lambda t: t.half().double()
+    P0 = h(pp[: 32 * width]).view(width, 32)
+    P1 = h(pp[32 * width:]).view(16, width)
+    a0 = h(enc) @ P0.T
+    pos_out = h(torch.relu(a0)) @ P1.T
+    sh = torch.from_numpy(ref_tcnn.sh(dirs.repeat_interleave(n_per_ray, 0).numpy(), 2))
+    x = torch.cat([h(sh), h(pos_out[:, 1:]), torch.ones(enc.shape[0], 13, dtype=torch.float64)], 1)
+    off, mins, hcur = 0, [a0.abs().min(1).values, pos_out[:, 0].abs()], x
+    dims = [32] + [width] * nhd + [16]
+    for k in range(nhd + 1):
+        Wk = h(pd[off: off + dims[k + 1] * dims[k]]).view(dims[k + 1], dims[k])
+        off += dims[k + 1] * dims[k]
+        a = hcur @ Wk.T
+        mins.append(a.abs().min(1).values if k < nhd else a[:, :4].abs().min(1).values)
+        hcur = h(torch.relu(a))
+    return torch.stack(mins, 1).min(1).values
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("width,nhd,R", [(64, 2, 29), (64, 2, 300), (32, 2, 29), (64, 1, 29),
+                                         (32, 1, 31)])
+def test_ingp_field_matches_oracle(dev, width, nhd, R):
+    """anr_ingp_field_{pack,fwd,bwd} == pos MLP -> SH2|pos_out[:,1:] -> dir MLP (oracle)."""
+    from atmonr_amd import _lib
+
+    nb, n_per_ray = 4, 37
+    M = n_per_ray * R
+    gen = torch.Generator().manual_seed(1000 * width + 10 * nhd + R)
+    pdsc = _lib.mlp_desc(32, 16, width, 1, False)
+    ddsc = _lib.mlp_desc(19, nb, width, nhd, False)
+    lib = _lib.load()
+    assert lib.anr_ingp_field_supported(ctypes.byref(pdsc), ctypes.byref(ddsc)) == 1
+    n_pp = lib.anr_mlp_n_params(ctypes.byref(pdsc))
+    n_pd = lib.anr_mlp_n_params(ctypes.byref(ddsc))
+    pp = torch.randn(n_pp, generator=gen) * (2.0 / 32) ** 0.5
+    pd = torch.randn(n_pd, generator=gen) * (2.0 / width) ** 0.5
+    enc = torch.rand(M, 32, generator=gen) * 2 - 1
+    dirs = torch.nn.functional.normalize(torch.randn(R, 3, generator=gen), dim=1)
+    for _ in range(40):  # keep every ReLU input away from 0 (f16 kernel vs f64 oracle)
+        tied = _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd) < 2e-3
+        if not tied.any():
+            break
+        enc[tied] = torch.rand(int(tied.sum()), 32, generator=gen) * 2 - 1
+    assert not tied.any()
+    enc_h = enc.half()
+    s = _lib.stream(dev)
+    pp_d, pd_d, enc_d, dirs_d = pp.to(dev), pd.to(dev), enc_h.to(dev), dirs.to(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(ctypes.byref(pdsc), ctypes.byref(ddsc)),
+                         device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", ctypes.byref(pdsc), ctypes.byref(ddsc), pp_d.data_ptr(),
+              pd_d.data_ptr(), packed.data_ptr(), s)
+    sigma = torch.empty(M, device=dev)
+    color = torch.empty(M, nb, device=dev)
+    _lib.call("anr_ingp_field_fwd", ctypes.byref(pdsc), ctypes.byref(ddsc), packed.data_ptr(),
+              enc_d.data_ptr(), 32, dirs_d.data_ptr(), n_per_ray, M, sigma.data_ptr(),
+              color.data_ptr(), nb, s)
+    e64 = enc_h.double().requires_grad_(True)
+    pr_p = pp.double().requires_grad_(True)
+    pr_d = pd.double().requires_grad_(True)
+    rs, rc, _, _ = _field_ref(e64, dirs, n_per_ray, pr_p, pr_d, width, nhd, nb)
+    close(sigma, rs.detach(), rel=1e-2, atol=1e-4)
+    close(color, rc.detach(), rel=1e-2, atol=1e-4)
+
+    dcol = torch.randn(M, nb, generator=gen) * 1e-2
+    dsig = torch.randn(M, generator=gen) * 1e-3
+    ((rc * dcol.double()).sum() + (rs * dsig.double()).sum()).backward()
+    dcol_d, dsig_d = dcol.to(dev), dsig.to(dev)
+    d_enc = torch.full((M, 32), float("nan"), device=dev)
+    g_pos = torch.full((n_pp,), 0.5, device=dev)  # accumulated into
+    g_dir = torch.full((n_pd,), -0.25, device=dev)
+    _lib.call("anr_ingp_field_bwd", ctypes.byref(pdsc), ctypes.byref(ddsc), packed.data_ptr(),
+              enc_d.data_ptr(), 32, dirs_d.data_ptr(), n_per_ray, M, dsig_d.data_ptr(),
+              dcol_d.data_ptr(), nb, d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), s)
+    close(d_enc, e64.grad, rel=2e-2, atol=1e-7)
+    close(g_pos - 0.5, pr_p.grad, rel=2e-2, atol=1e-7)
+    close(g_dir + 0.25, pr_d.grad, rel=2e-2, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_ingp_field_unsupported_and_empty(dev):
+    from atmonr_amd import _lib
+
+    lib = _lib.load()
+    pdsc = _lib.mlp_desc(32, 16, 64, 1, False)
+    assert lib.anr_ingp_field_supported(ctypes.byref(pdsc),
+                                        ctypes.byref(_lib.mlp_desc(19, 4, 64, 3, False))) == 0
+    assert lib.anr_ingp_field_supported(ctypes.byref(_lib.mlp_desc(24, 16, 64, 1, False)),
+                                        ctypes.byref(_lib.mlp_desc(19, 4, 64, 2, False))) == 0
+    ddsc = _lib.mlp_desc(19, 4, 64, 2, False)
+    rc = lib.anr_ingp_field_fwd(ctypes.byref(pdsc), ctypes.byref(_lib.mlp_desc(19, 4, 64, 3, False)),
+                                None, None, 32, None, 1, 10, None, None, 4, None)
+    assert rc == -1 and b"unsupported" in lib.anr_last_error()
+    assert lib.anr_ingp_field_fwd(ctypes.byref(pdsc), ctypes.byref(ddsc), None, None, 32, None,
+                                  1, 0, None, None, 4, None) == 0

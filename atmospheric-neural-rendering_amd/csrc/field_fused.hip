@@ -23,10 +23,34 @@
 // per wavefront (pre-pass over |dL/dcolor| and |dL/dsigma|) and unscaled in f32.
 // dL/dpos_out never leaves the registers; the kernel writes only dL/denc (f32).
 
+#include <type_traits>
+
 #include "anr_common.h"
+
+// Profiling ablations (tools/field_ablate.sh); 0 in every product build. Bits:
+// 1 no dW MFMAs, 2 no layer-input stores, 4 no gradient-tile stores, 8 no mask reads.
+#ifndef FIELD_EXP
+#define FIELD_EXP 0
+#endif
 
 namespace anr {
 namespace field {
+
+#ifdef FIELD_STAMP
+// per-stage cycle totals of wavefront 0 of the backward (s_memtime), debug builds only
+__device__ unsigned long long g_stamp[16];
+#define STAMP(k)                                                             \
+  do {                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    unsigned long long t_;                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));        \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    if (stamp_on) { st_acc[k] += t_ - st_last; }                             \
+    st_last = t_;                                                            \
+  } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
 
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -36,6 +60,16 @@ typedef __attribute__((address_space(3))) s4v lds_s4v;
 
 __device__ __forceinline__ f4 mma32(h8 a, h8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// dW accumulation: the accumulator lives in AGPRs for the whole kernel (the rest of the
+// kernel's MFMAs write VGPRs). The compiler does not see these as MFMAs, so every VALU
+// access to an accumulator goes through agpr_fence() first (result-latency wait states).
+__device__ __forceinline__ void mma32_acc(f4& acc, h8 a, h8 b) {
+  if constexpr ((FIELD_EXP & 1) != 0) return;
+  asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void agpr_fence() {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 }
 __device__ __forceinline__ f4 mma16(h4 a, h4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
@@ -85,9 +119,9 @@ struct Net {
   static constexpr int oXde = oXph + 32 * LH;     // dir input (k') [32][LX]
   static constexpr int oXd0 = oXde + 32 * LX;     // dir hidden 0   [32][LH]
   static constexpr int oXd1 = oXd0 + 32 * LH;     // dir hidden 1   [32][LH] (NHD == 2)
-  static constexpr int oGa = oXd1 + (NHD - 1) * 32 * LH;
-  static constexpr int oGb = oGa + 32 * LH;
-  static constexpr int wave_lds = oGb + 32 * LH;
+  static constexpr int wave_x = oXd1 + (NHD - 1) * 32 * LH;  // layer-input tiles
+  static constexpr int oGa = 0, oGb = 32 * LH, wave_g = 2 * 32 * LH;  // gradient tiles
+  static constexpr int wave_lds = wave_x + wave_g;
 };
 
 // ---------------------------------------------------------------------------------
@@ -176,48 +210,77 @@ struct Args {
 __device__ __forceinline__ h8 cat(h4 a, h4 b) {
   return h8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 }
+// f32 accumulators -> f16 (round to nearest even, v_cvt_pk_f16_f32) -> ReLU (v_pk_max_f16)
 __device__ __forceinline__ h4 relu_h4(f4 v) {
-  return h4{static_cast<_Float16>(fmaxf(v[0], 0.0f)), static_cast<_Float16>(fmaxf(v[1], 0.0f)),
-            static_cast<_Float16>(fmaxf(v[2], 0.0f)), static_cast<_Float16>(fmaxf(v[3], 0.0f))};
+  const h4 x = __builtin_convertvector(v, h4);
+  return __builtin_elementwise_max(x, h4{0, 0, 0, 0});
 }
-__device__ __forceinline__ h4 to_h4(f4 v) {
-  return h4{static_cast<_Float16>(v[0]), static_cast<_Float16>(v[1]),
-            static_cast<_Float16>(v[2]), static_cast<_Float16>(v[3])};
+__device__ __forceinline__ h4 to_h4(f4 v) { return __builtin_convertvector(v, h4); }
+// ReLU derivative: keep g where the forward activation (>= 0, f16) is nonzero. On the bits:
+// v_pk_min_u16(act, 1) is 0 or 1 per half and v_pk_mul_lo_u16 by it keeps or clears g
+// (two instructions per pair; written as asm because the compiler expands it to selects).
+__device__ __forceinline__ uint32_t mask2(uint32_t g, uint32_t act) {
+  uint32_t m, r;
+  // op_sel_hi:[1,0]: the high half of the constant operand also reads its low 16 bits (= 1)
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(m) : "v"(act));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(g), "v"(m));
+  return r;
 }
-// zero where the forward activation was not positive (ReLU derivative)
 __device__ __forceinline__ h4 mask_h4(f4 g, h4 act) {
-  return h4{static_cast<_Float16>(act.x > static_cast<_Float16>(0) ? g[0] : 0.0f),
-            static_cast<_Float16>(act.y > static_cast<_Float16>(0) ? g[1] : 0.0f),
-            static_cast<_Float16>(act.z > static_cast<_Float16>(0) ? g[2] : 0.0f),
-            static_cast<_Float16>(act.w > static_cast<_Float16>(0) ? g[3] : 0.0f)};
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  const u2 gb = __builtin_bit_cast(u2, to_h4(g)), ab = __builtin_bit_cast(u2, act);
+  return __builtin_bit_cast(h4, u2{mask2(gb.x, ab.x), mask2(gb.y, ab.y)});
 }
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+// Global inputs of one 16-sample half-tile for this lane, loaded a tile ahead.
+struct Rows {
+  h8 xe;          // enc[row][8g .. 8g+7]
+  float dx, dy, dz;  // direction of the row's ray, remapped 2d-1 (g == 0 lanes)
+  f4 dc;          // dL/dcolor[row][4g .. 4g+3] (backward)
+  float ds;       // dL/dsigma[row] (backward, g == 0 lanes)
+};
 
-// Input row of the dir MLP for the sample in this lane (B-operand slots 8g..8g+7).
-__device__ __forceinline__ h8 dir_input(const Args& a, int64_t row, int g, f4 po) {
-  if (row >= a.M) return h8{};
-  h8 x;
+__device__ __forceinline__ void load_rows(const Args& a, int64_t row, int g, bool bwd, Rows& in) {
+  in.xe = h8{};
+  in.dx = in.dy = in.dz = 0.0f;
+  in.dc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  in.ds = 0.0f;
+  if (row >= a.M) return;
+  in.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
   if (g == 0) {
     const uint32_t ray = static_cast<uint32_t>(row) / a.n_per_ray;
     const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
-    const float dx = d[0] * 2.0f - 1.0f, dy = d[1] * 2.0f - 1.0f, dz = d[2] * 2.0f - 1.0f;
-    x = h8{static_cast<_Float16>(1.0f), static_cast<_Float16>(po[1]),
-           static_cast<_Float16>(po[2]), static_cast<_Float16>(po[3]),
-           static_cast<_Float16>(0.28209479177387814f),
-           static_cast<_Float16>(-0.48860251190291987f * dy),
-           static_cast<_Float16>(0.48860251190291987f * dz),
-           static_cast<_Float16>(-0.48860251190291987f * dx)};
-  } else {
-    const _Float16 one = static_cast<_Float16>(1.0f);
-    x = h8{static_cast<_Float16>(po[0]), static_cast<_Float16>(po[1]),
-           static_cast<_Float16>(po[2]), static_cast<_Float16>(po[3]), one, one, one, one};
+    in.dx = d[0] * 2.0f - 1.0f;
+    in.dy = d[1] * 2.0f - 1.0f;
+    in.dz = d[2] * 2.0f - 1.0f;
+    if (bwd && a.d_sigma) in.ds = a.d_sigma[row];
   }
-  return x;
+  if (bwd) {
+    const int c0 = 4 * g;
+    const float* dcp = a.d_color + row * a.d_color_stride + c0;
+    if (c0 + 3 < a.n_out && (a.d_color_stride & 3) == 0) {
+      in.dc = *reinterpret_cast<const f4*>(dcp);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (c0 + i < a.n_out) in.dc[i] = dcp[i];
+    }
+  }
+}
+
+// Input row of the dir MLP for the sample in this lane (B-operand slots 8g..8g+7).
+__device__ __forceinline__ h8 dir_input(const Rows& in, bool valid, int g, f4 po) {
+  if (!valid) return h8{};
+  if (g == 0)
+    return h8{static_cast<_Float16>(1.0f), static_cast<_Float16>(po[1]),
+              static_cast<_Float16>(po[2]), static_cast<_Float16>(po[3]),
+              static_cast<_Float16>(0.28209479177387814f),
+              static_cast<_Float16>(-0.48860251190291987f * in.dy),
+              static_cast<_Float16>(0.48860251190291987f * in.dz),
+              static_cast<_Float16>(-0.48860251190291987f * in.dx)};
+  const _Float16 one = static_cast<_Float16>(1.0f);
+  return h8{static_cast<_Float16>(po[0]), static_cast<_Float16>(po[1]),
+            static_cast<_Float16>(po[2]), static_cast<_Float16>(po[3]), one, one, one, one};
 }
 
 template <int W, int NHD>
@@ -239,9 +302,29 @@ struct FwdWeights {
 #pragma unroll
     for (int i = 0; i < N::KB; ++i) d2[i] = ld(N::oFD2 + i * N::F32);
   }
+  __device__ h8 P0(int i) const { return p0[i]; }
+  __device__ h8 P1(int i) const { return p1[i]; }
+  __device__ h8 D0(int i) const { return d0[i]; }
+  __device__ h8 D1(int i) const { return d1[i]; }
+  __device__ h8 D2(int i) const { return d2[i]; }
 };
 
-// Forward of one 16-sample tile; every intermediate the backward needs is returned.
+// The same fragments read from a packed copy in LDS (backward kernel).
+template <int W, int NHD>
+struct LdsWeights {
+  using N = Net<W, NHD>;
+  const _Float16* base;
+  int lane;
+  __device__ h8 frag(int off) const { return *reinterpret_cast<const h8*>(base + off + lane * 8); }
+  __device__ h8 P0(int i) const { return frag(N::oFP0 + i * N::F32); }
+  __device__ h8 P1(int i) const { return frag(N::oFP1 + i * N::F32); }
+  __device__ h8 D0(int i) const { return frag(N::oFD0 + i * N::F32); }
+  __device__ h8 D1(int i) const { return frag(N::oFD1 + i * N::F32); }
+  __device__ h8 D2(int i) const { return frag(N::oFD2 + i * N::F32); }
+};
+
+// Forward of NM 16-sample tiles, layer by layer across the tiles (independent MFMAs back
+// to back, so no result is consumed right after the instruction that produces it).
 template <int W, int NHD>
 struct Tile {
   using N = Net<W, NHD>;
@@ -250,52 +333,108 @@ struct Tile {
   f4 po, col;
 };
 
-template <int W, int NHD>
-__device__ __forceinline__ void tile_forward(const Args& a, const FwdWeights<W, NHD>& fw,
-                                             int64_t row, int g, Tile<W, NHD>& t) {
+struct NoSink {
+  __device__ void xe(int, h8) const {}
+  __device__ void xd(int, h8) const {}
+  __device__ void hp(int, int, h4) const {}
+  __device__ void hd0(int, int, h4) const {}
+  __device__ void hd1(int, int, h4) const {}
+};
+
+// sink: receives every layer input as soon as it is computed (the backward writes them
+// to LDS there, so they need not stay live in registers)
+template <int W, int NHD, int NM, typename WS, typename SK>
+__device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const bool* valid,
+                                             int g, Tile<W, NHD>* t, const SK& sink) {
   using N = Net<W, NHD>;
-  t.xe = h8{};
-  if (row < a.M) t.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int nt = 0; nt < N::NT; ++nt)
-    t.hp[nt] = relu_h4(mma32(fw.p0[nt], t.xe, f4{0.0f, 0.0f, 0.0f, 0.0f}));
-  t.po = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  for (int mt = 0; mt < NM; ++mt) {
+    t[mt].xe = in[mt].xe;
+    sink.xe(mt, t[mt].xe);
+  }
 #pragma unroll
-  for (int kb = 0; kb < N::KB; ++kb) t.po = mma32(fw.p1[kb], cat(t.hp[2 * kb], t.hp[2 * kb + 1]), t.po);
-  t.xd = dir_input(a, row, g, t.po);
+  for (int nt = 0; nt < N::NT; ++nt) {
+    const h8 w = fw.P0(nt);
 #pragma unroll
-  for (int nt = 0; nt < N::NT; ++nt)
-    t.hd0[nt] = relu_h4(mma32(fw.d0[nt], t.xd, f4{0.0f, 0.0f, 0.0f, 0.0f}));
-  const h4* last = t.hd0;
+    for (int mt = 0; mt < NM; ++mt) {
+      t[mt].hp[nt] = relu_h4(mma32(w, t[mt].xe, z4));
+      sink.hp(mt, nt, t[mt].hp[nt]);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < NM; ++mt) t[mt].po = z4;
+#pragma unroll
+  for (int kb = 0; kb < N::KB; ++kb) {
+    const h8 w = fw.P1(kb);
+#pragma unroll
+    for (int mt = 0; mt < NM; ++mt) t[mt].po = mma32(w, cat(t[mt].hp[2 * kb], t[mt].hp[2 * kb + 1]), t[mt].po);
+  }
+#pragma unroll
+  for (int mt = 0; mt < NM; ++mt) {
+    t[mt].xd = dir_input(in[mt], valid[mt], g, t[mt].po);
+    sink.xd(mt, t[mt].xd);
+  }
+#pragma unroll
+  for (int nt = 0; nt < N::NT; ++nt) {
+    const h8 w = fw.D0(nt);
+#pragma unroll
+    for (int mt = 0; mt < NM; ++mt) {
+      t[mt].hd0[nt] = relu_h4(mma32(w, t[mt].xd, z4));
+      sink.hd0(mt, nt, t[mt].hd0[nt]);
+    }
+  }
   if constexpr (NHD == 2) {
 #pragma unroll
     for (int nt = 0; nt < N::NT; ++nt) {
-      f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      f4 acc[NM];
 #pragma unroll
-      for (int kb = 0; kb < N::KB; ++kb)
-        acc = mma32(fw.d1[nt * N::KB + kb], cat(t.hd0[2 * kb], t.hd0[2 * kb + 1]), acc);
-      t.hd1[nt] = relu_h4(acc);
+      for (int mt = 0; mt < NM; ++mt) acc[mt] = z4;
+#pragma unroll
+      for (int kb = 0; kb < N::KB; ++kb) {
+        const h8 w = fw.D1(nt * N::KB + kb);
+#pragma unroll
+        for (int mt = 0; mt < NM; ++mt)
+          acc[mt] = mma32(w, cat(t[mt].hd0[2 * kb], t[mt].hd0[2 * kb + 1]), acc[mt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < NM; ++mt) {
+        t[mt].hd1[nt] = relu_h4(acc[mt]);
+        sink.hd1(mt, nt, t[mt].hd1[nt]);
+      }
     }
-    last = t.hd1;
   }
-  t.col = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int kb = 0; kb < N::KB; ++kb) t.col = mma32(fw.d2[kb], cat(last[2 * kb], last[2 * kb + 1]), t.col);
+  for (int mt = 0; mt < NM; ++mt) t[mt].col = z4;
+#pragma unroll
+  for (int kb = 0; kb < N::KB; ++kb) {
+    const h8 w = fw.D2(kb);
+#pragma unroll
+    for (int mt = 0; mt < NM; ++mt) {
+      const h4* last = NHD == 2 ? t[mt].hd1 : t[mt].hd0;
+      t[mt].col = mma32(w, cat(last[2 * kb], last[2 * kb + 1]), t[mt].col);
+    }
+  }
 }
 
 template <int W, int NHD>
 __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
-  using N = Net<W, NHD>;
   const int lane = threadIdx.x & 63, g = lane >> 4;
   const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
   FwdWeights<W, NHD> fw;
   fw.load(a.packed, lane);
   const int64_t n_tiles = (a.M + 15) / 16;
-  for (int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave; tile < n_tiles;
-       tile += static_cast<int64_t>(gridDim.x) * waves) {
+  const int64_t tstride = static_cast<int64_t>(gridDim.x) * waves;
+  int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave;
+  Rows cur;
+  load_rows(a, tile * 16 + (lane & 15), g, false, cur);
+  for (; tile < n_tiles; tile += tstride) {
     const int64_t row = tile * 16 + (lane & 15);
+    Rows nxt;  // next tile's inputs in flight while this one computes
+    load_rows(a, (tile + tstride) * 16 + (lane & 15), g, false, nxt);
     Tile<W, NHD> t;
-    tile_forward<W, NHD>(a, fw, row, g, t);
+    const bool valid = row < a.M;
+    tile_forward<W, NHD, 1>(fw, &cur, &valid, g, &t, NoSink{});
     if (row < a.M) {
       if (g == 0) a.sigma[row] = fmaxf(t.po[0], 0.0f);
       const int c0 = 4 * g;
@@ -310,6 +449,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
           if (c0 + i < a.n_out) a.color[row * a.color_stride + c0 + i] = fmaxf(t.col[i], 0.0f);
       }
     }
+    cur = nxt;
   }
 }
 
@@ -324,62 +464,119 @@ __device__ __forceinline__ h8 tr_read(const _Float16* base, int ld, int col0, in
   return cat(__builtin_bit_cast(h4, v0), __builtin_bit_cast(h4, v1));
 }
 
+// C-layout (sample l&15, units 4g..4g+3) read back from row `mrow` of a row-major tile
+__device__ __forceinline__ h4 ld4(const _Float16* base, int ld, int mrow, int col) {
+  if constexpr ((FIELD_EXP & 8) != 0) return h4{1, 1, 1, 1};
+  return *reinterpret_cast<const h4*>(base + mrow * ld + col);
+}
+
 // C-layout (sample l&15, units 4g..4g+3) store into row `mrow` of a row-major tile
 __device__ __forceinline__ void st4(_Float16* base, int ld, int mrow, int col, h4 v) {
   *reinterpret_cast<h4*>(base + mrow * ld + col) = v;
 }
+// gradient-tile store (ablation bit 4)
+__device__ __forceinline__ void st4g(_Float16* base, int ld, int mrow, int col, h4 v) {
+  if constexpr ((FIELD_EXP & 4) != 0) return;
+  *reinterpret_cast<h4*>(base + mrow * ld + col) = v;
+}
 
-template <int W, int NHD>
-__global__ void __launch_bounds__(256) bwd_kernel(Args a, float target) {
-  using N = Net<W, NHD>;
-  constexpr int NT = N::NT, KB = N::KB, LX = N::LX, LH = N::LH;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  _Float16* wb = reinterpret_cast<_Float16*>(smem);  // backward fragments, N::n_bwd halves
-  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
-  const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
-  for (int e = threadIdx.x * 8; e < N::n_bwd; e += blockDim.x * 8)
-    *reinterpret_cast<h8*>(wb + e) = *reinterpret_cast<const h8*>(a.packed + N::n_fwd + e);
-  _Float16* L = wb + N::n_bwd + wave * N::wave_lds;
-  _Float16* Xpe = L + N::oXpe;
-  _Float16* Xph = L + N::oXph;
-  _Float16* Xde = L + N::oXde;
-  _Float16* Xd0 = L + N::oXd0;
-  _Float16* Xd1 = L + N::oXd1;
-  _Float16* Ga = L + N::oGa;
-  _Float16* Gb = L + N::oGb;
-  _Float16* Xlast = NHD == 2 ? Xd1 : Xd0;
-  FwdWeights<W, NHD> fw;
-  fw.load(a.packed, lane);
-  __syncthreads();
-  auto bfrag32 = [&](int off) { return *reinterpret_cast<const h8*>(wb + (off - N::n_fwd) + lane * 8); };
-  auto bfrag16 = [&](int off) { return *reinterpret_cast<const h4*>(wb + (off - N::n_fwd) + lane * 4); };
-
-  const int64_t n_tiles = (a.M + 31) / 32;
-  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * waves + wave;
-  const int64_t tstride = static_cast<int64_t>(gridDim.x) * waves;
-
-  // per-wavefront gradient scale: max(|dL/dcolor|, |dL/dsigma|) over this wave's rows -> target
-  float s = 1.0f, inv_s = 1.0f;
-  {
-    float gmax = 0.0f;
-    for (int64_t tile = t0; tile < n_tiles; tile += tstride) {
-      const int64_t row = tile * 32 + (lane & 31);
-      if (row < a.M) {
-        const int half = lane >> 5;  // two lanes per row: columns split
-        for (int c = half; c < a.n_out; c += 2)
-          gmax = fmaxf(gmax, fabsf(a.d_color[row * a.d_color_stride + c]));
-        if (half == 0 && a.d_sigma) gmax = fmaxf(gmax, fabsf(a.d_sigma[row]));
-      }
+// Rows of the backward's wavefront w: tiles [w*tpw, (w+1)*tpw) of 32 rows. The f16
+// gradient scale of a wavefront is set from max(|dL/dcolor|, |dL/dsigma|) over its rows,
+// which this kernel computes first (one block per wavefront range, full occupancy).
+__global__ void __launch_bounds__(256) absmax_kernel(Args a, int64_t rows_per_wave, float* wmax) {
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_wave;
+  const int64_t r1 = r0 + rows_per_wave < a.M ? r0 + rows_per_wave : a.M;
+  float m = 0.0f;
+  if (a.n_out == 4 && (a.d_color_stride & 3) == 0) {
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+      const f4 d = *reinterpret_cast<const f4*>(a.d_color + r * a.d_color_stride);
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
+      if (a.d_sigma) m = fmaxf(m, fabsf(a.d_sigma[r]));
     }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) gmax = fmaxf(gmax, __shfl_xor(gmax, m));
-    if (gmax > 0.0f) {
-      int e2 = static_cast<int>(floorf(log2f(target / gmax)));
-      e2 = e2 < -60 ? -60 : (e2 > 100 ? 100 : e2);
-      s = ldexpf(1.0f, e2);
-      inv_s = ldexpf(1.0f, -e2);
+  } else {
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+      for (int c = 0; c < a.n_out; ++c) m = fmaxf(m, fabsf(a.d_color[r * a.d_color_stride + c]));
+      if (a.d_sigma) m = fmaxf(m, fabsf(a.d_sigma[r]));
     }
   }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < static_cast<int>(blockDim.x >> 6); ++i) m = fmaxf(m, part[i]);
+    wmax[blockIdx.x] = m;
+  }
+}
+
+// Raw global inputs of one 16-sample half-tile of a FULL tile in the FAST case (n_out == 4,
+// aligned d_color rows, d_sigma present), prefetched a tile ahead. Nothing is computed
+// on the loaded values here — any use would make the compiler wait for the load right
+// away; raw_to_rows() converts them one tile later. Every lane loads its row's direction,
+// d_sigma and d_color (same addresses across the lane groups: no extra traffic).
+struct RawRows {
+  h8 xe;
+  float d0, d1, d2, ds;
+  f4 dc;
+};
+
+__device__ __forceinline__ void load_raw(const Args& a, int64_t row, int g, RawRows& r) {
+  r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+  const uint32_t ray = static_cast<uint32_t>(row) / a.n_per_ray;
+  const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
+  r.d0 = d[0];
+  r.d1 = d[1];
+  r.d2 = d[2];
+  r.ds = a.d_sigma[row];
+  r.dc = *reinterpret_cast<const f4*>(a.d_color + row * a.d_color_stride);
+}
+
+__device__ __forceinline__ void raw_to_rows(const RawRows& r, int g, Rows& in) {
+  in.xe = r.xe;
+  in.dx = r.d0 * 2.0f - 1.0f;
+  in.dy = r.d1 * 2.0f - 1.0f;
+  in.dz = r.d2 * 2.0f - 1.0f;
+  in.ds = r.ds;
+  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+  in.dc = g == 0 ? r.dc : z4;
+}
+
+template <int W, int NHD, bool FAST>
+__global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t tpw,
+                                                  const float* wmax) {
+  using N = Net<W, NHD>;
+  constexpr int NT = N::NT, KB = N::KB, LX = N::LX, LH = N::LH;
+  // Three separate LDS objects, so alias analysis can tell weight-fragment reads, layer-
+  // input tiles and gradient tiles apart and keep reads in flight across the others' stores.
+  __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
+  __shared__ __attribute__((aligned(16))) _Float16 xsm[4][N::wave_x];
+  __shared__ __attribute__((aligned(16))) _Float16 gsm[4][N::wave_g];
+  _Float16* wb = wsm;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
+  for (int e = threadIdx.x * 8; e < N::n_packed; e += blockDim.x * 8)
+    *reinterpret_cast<h8*>(wb + e) = *reinterpret_cast<const h8*>(a.packed + e);
+  _Float16* Xpe = xsm[wave] + N::oXpe;
+  _Float16* Xph = xsm[wave] + N::oXph;
+  _Float16* Xde = xsm[wave] + N::oXde;
+  _Float16* Xd0 = xsm[wave] + N::oXd0;
+  _Float16* Xd1 = xsm[wave] + N::oXd1;
+  _Float16* Ga = gsm[wave] + N::oGa;
+  _Float16* Gb = gsm[wave] + N::oGb;
+  _Float16* Xlast = NHD == 2 ? Xd1 : Xd0;
+  __syncthreads();
+  // wbt: per-tile opaque copy of the fragment base, so the compiler re-reads the weight
+  // fragments from LDS each tile instead of hoisting them into registers
+  const _Float16* wbt = wb;
+  auto bfrag32 = [&](int off) { return *reinterpret_cast<const h8*>(wbt + off + lane * 8); };
+  auto bfrag16 = [&](int off) { return *reinterpret_cast<const h4*>(wbt + off + lane * 4); };
+
+  const int64_t n_tiles = (a.M + 31) / 32;
+  const int64_t w_id = static_cast<int64_t>(blockIdx.x) * waves + wave;
+  const int64_t t_begin = w_id * tpw;
+  const int64_t t_end = t_begin + tpw < n_tiles ? t_begin + tpw : n_tiles;
+  const int64_t n_full = a.M / 32;  // tiles with all 32 rows in range
 
   f4 dD2[NT], dD1[NHD == 2 ? NT * NT : 1], dD0[NT * 2], dP1[NT], dP0[NT * 2];
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -391,173 +588,264 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target) {
 #pragma unroll
     for (int i = 0; i < NT * NT; ++i) dD1[i] = z4;
   }
+  // f16 gradient scale 2^e of this wavefront (max over its rows -> target); the dW
+  // accumulators are never touched by VALU inside the tile loop (they stay in AGPRs)
+  float s = 1.0f, inv_s = 1.0f;
+  {
+    const float gm = t_begin < t_end ? wmax[w_id] : 0.0f;
+    if (gm > 0.0f) {
+      int e = static_cast<int>(floorf(log2f(target / gm)));
+      e = e < -60 ? -60 : (e > 100 ? 100 : e);
+      s = ldexpf(1.0f, e);
+      inv_s = ldexpf(1.0f, -e);
+    }
+  }
 
-  for (int64_t tile = t0; tile < n_tiles; tile += tstride) {
-    Tile<W, NHD> t[2];
+  Rows cur[2];
+  RawRows nraw[2];
+  const int64_t t_full_end = t_end < n_full ? t_end : n_full;
+  if constexpr (FAST) {
+    if (t_begin < t_full_end) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) load_raw(a, t_begin * 32 + mt * 16 + li, g, nraw[mt]);
+    }
+  }
+#ifdef FIELD_STAMP
+  const bool stamp_on = w_id == 0;
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+  {
+    unsigned long long t_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));
+    st_last = t_;
+  }
+#endif
+  // one tile; FULL: all 32 rows in range (no bounds checks, one basic block)
+  auto process = [&](auto full_c, int64_t tile) {
+    constexpr bool FULL = decltype(full_c)::value;
+    {
+      int zoff = 0;
+      asm volatile("" : "+v"(zoff));
+      wbt = wb + zoff;
+    }
+    if constexpr (FAST && FULL) {
+      // this tile's inputs arrived during the previous tile; issue the next tile's now
+      // (clamped to the last full tile: always a valid address, no branch)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) raw_to_rows(nraw[mt], g, cur[mt]);
+      const int64_t tn = tile + 1 < t_full_end ? tile + 1 : tile;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) load_raw(a, tn * 32 + mt * 16 + li, g, nraw[mt]);
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) load_rows(a, tile * 32 + mt * 16 + li, g, true, cur[mt]);
+    }
+    const bool full = FULL;
+    STAMP(0);
     h4 gc[2];
     bool dens[2];
-    // ---- recompute the forward for both 16-sample halves, write layer inputs to LDS
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const int64_t row = tile * 32 + mt * 16 + li;
-      const int m = mt * 16 + li;
-      tile_forward<W, NHD>(a, fw, row, g, t[mt]);
-      *reinterpret_cast<h8*>(Xpe + m * LX + 8 * g) = t[mt].xe;
-      *reinterpret_cast<h8*>(Xde + m * LX + 8 * g) = t[mt].xd;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        st4(Xph, LH, m, 16 * nt + 4 * g, t[mt].hp[nt]);
-        st4(Xd0, LH, m, 16 * nt + 4 * g, t[mt].hd0[nt]);
-        if constexpr (NHD == 2) st4(Xd1, LH, m, 16 * nt + 4 * g, t[mt].hd1[nt]);
-      }
-      dens[mt] = t[mt].po[0] > 0.0f;
-      // dL/d(color pre-activation), scaled
-      f4 gv = z4;
-      if (row < a.M) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = 4 * g + i;
-          if (c < a.n_out && t[mt].col[i] > 0.0f) gv[i] = a.d_color[row * a.d_color_stride + c] * s;
-        }
-      }
-      gc[mt] = to_h4(gv);
-      st4(Ga, LH, m, 4 * g, gc[mt]);
-    }
-    wave_sync();
-    // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
+    // ---- recompute the forward for both 16-sample halves; every layer input goes to LDS
+    // as soon as it is computed (the backward's ReLU masks are read back from there)
     {
-      const h8 ga = tr_read(Ga, LH, 0, lane);
+      Tile<W, NHD> t[2];
+      bool valid[2];
 #pragma unroll
-      for (int kt = 0; kt < NT; ++kt) dD2[kt] = mma32(ga, tr_read(Xlast, LH, 16 * kt, lane), dD2[kt]);
-    }
-    h4 dl[2][NT];
-#pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
-      const h4 wf = bfrag16(N::oBD2 + kt * N::F16);
+      for (int mt = 0; mt < 2; ++mt) valid[mt] = full || tile * 32 + mt * 16 + li < a.M;
+      struct Sink {
+        _Float16 *Xpe, *Xde, *Xph, *Xd0, *Xd1;
+        int li, g;
+        __device__ void xe(int mt, h8 v) const { if constexpr ((FIELD_EXP & 2) == 0) *reinterpret_cast<h8*>(Xpe + (mt * 16 + li) * LX + 8 * g) = v; }
+        __device__ void xd(int mt, h8 v) const { if constexpr ((FIELD_EXP & 2) == 0) *reinterpret_cast<h8*>(Xde + (mt * 16 + li) * LX + 8 * g) = v; }
+        __device__ void hp(int mt, int nt, h4 v) const { if constexpr ((FIELD_EXP & 2) == 0) st4(Xph, LH, mt * 16 + li, 16 * nt + 4 * g, v); }
+        __device__ void hd0(int mt, int nt, h4 v) const { if constexpr ((FIELD_EXP & 2) == 0) st4(Xd0, LH, mt * 16 + li, 16 * nt + 4 * g, v); }
+        __device__ void hd1(int mt, int nt, h4 v) const { if constexpr ((FIELD_EXP & 2) == 0) st4(Xd1, LH, mt * 16 + li, 16 * nt + 4 * g, v); }
+      };
+      // all forward fragments in flight at once, then the five layers
+      FwdWeights<W, NHD> fwl;
+      fwl.load(wbt, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      tile_forward<W, NHD, 2>(fwl, cur, valid, g, t, Sink{Xpe, Xde, Xph, Xd0, Xd1, li, g});
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const f4 acc = mma16(wf, gc[mt], z4);
-        dl[mt][kt] = mask_h4(acc, NHD == 2 ? t[mt].hd1[kt] : t[mt].hd0[kt]);
-        st4(Gb, LH, mt * 16 + li, 16 * kt + 4 * g, dl[mt][kt]);
+        dens[mt] = t[mt].po[0] > 0.0f;
+        f4 gv;  // dL/d(color pre-activation), scaled (cur.dc is zero outside g == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gv[i] = t[mt].col[i] > 0.0f ? cur[mt].dc[i] * s : 0.0f;
+        gc[mt] = to_h4(gv);
+        st4g(Ga, LH, mt * 16 + li, 4 * g, gc[mt]);
       }
     }
-    wave_sync();
+    STAMP(1);
+    // Each stage below first issues every LDS read it needs (weight fragments, ReLU masks,
+    // transposed tiles), then a scheduling barrier, then its MFMAs: one LDS round trip
+    // per stage instead of one per MFMA group.
+    // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
+    h4 dl[2][NT];
+    {
+      const h8 ga = tr_read(Ga, LH, 0, lane);
+      h8 xl[NT];
+      h4 wf[NT], mk[2][NT];
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        xl[kt] = tr_read(Xlast, LH, 16 * kt, lane);
+        wf[kt] = bfrag16(N::oBD2 + kt * N::F16);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xlast, LH, mt * 16 + li, 16 * kt + 4 * g);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) mma32_acc(dD2[kt], ga, xl[kt]);
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          dl[mt][kt] = mask_h4(mma16(wf[kt], gc[mt], z4), mk[mt][kt]);
+          st4g(Gb, LH, mt * 16 + li, 16 * kt + 4 * g, dl[mt][kt]);
+        }
+      }
+    }
+    STAMP(2);
     // ---- dir hidden layer 1 (NHD == 2): dW_D1 (W x W) += dl^T · X_d0 ; dh0 = D1^T dl
     h4 dh0[2][NT];
     _Float16* Gdh0 = Gb;
     if constexpr (NHD == 2) {
-      h8 xb[NT];
+      h8 xb[NT], gb[NT], wf[NT * KB];
+      h4 mk[2][NT];
 #pragma unroll
-      for (int kt = 0; kt < NT; ++kt) xb[kt] = tr_read(Xd0, LH, 16 * kt, lane);
+      for (int kt = 0; kt < NT; ++kt) {
+        xb[kt] = tr_read(Xd0, LH, 16 * kt, lane);
+        gb[kt] = tr_read(Gb, LH, 16 * kt, lane);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const h8 ga = tr_read(Gb, LH, 16 * nt, lane);
+        for (int kb = 0; kb < KB; ++kb) wf[kt * KB + kb] = bfrag32(N::oBD1 + (kt * KB + kb) * N::F32);
 #pragma unroll
-        for (int kt = 0; kt < NT; ++kt) dD1[nt * NT + kt] = mma32(ga, xb[kt], dD1[nt * NT + kt]);
+        for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xd0, LH, mt * 16 + li, 16 * kt + 4 * g);
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int kt = 0; kt < NT; ++kt) mma32_acc(dD1[nt * NT + kt], gb[nt], xb[kt]);
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
         f4 acc[2] = {z4, z4};
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          const h8 wf = bfrag32(N::oBD1 + (kt * KB + kb) * N::F32);
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf, cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
-        }
+          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf[kt * KB + kb], cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          dh0[mt][kt] = mask_h4(acc[mt], t[mt].hd0[kt]);
-          st4(Ga, LH, mt * 16 + li, 16 * kt + 4 * g, dh0[mt][kt]);
+          dh0[mt][kt] = mask_h4(acc[mt], mk[mt][kt]);
+          st4g(Ga, LH, mt * 16 + li, 16 * kt + 4 * g, dh0[mt][kt]);
         }
       }
       Gdh0 = Ga;
-      wave_sync();
     } else {
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) dh0[mt][kt] = dl[mt][kt];
     }
-    _Float16* Gfree = Gdh0 == Ga ? Gb : Ga;
+    _Float16* Gfree = NHD == 2 ? Gb : Ga;
+    STAMP(3);
     // ---- dir input layer: dW_D0 (W x 32, k' order) += dh0^T · X_de ; dpos = D0^T dh0
-    {
-      const h8 x0 = tr_read(Xde, LX, 0, lane), x1 = tr_read(Xde, LX, 16, lane);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const h8 ga = tr_read(Gdh0, LH, 16 * nt, lane);
-        dD0[nt * 2] = mma32(ga, x0, dD0[nt * 2]);
-        dD0[nt * 2 + 1] = mma32(ga, x1, dD0[nt * 2 + 1]);
-      }
-    }
     h4 dpo[2];
     {
+      const h8 x0 = tr_read(Xde, LX, 0, lane), x1 = tr_read(Xde, LX, 16, lane);
+      h8 gd[NT], wf[KB];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) gd[nt] = tr_read(Gdh0, LH, 16 * nt, lane);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) wf[kb] = bfrag32(N::oBD0 + kb * N::F32);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        mma32_acc(dD0[nt * 2], gd[nt], x0);
+        mma32_acc(dD0[nt * 2 + 1], gd[nt], x1);
+      }
       f4 acc[2] = {z4, z4};
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        const h8 wf = bfrag32(N::oBD0 + kb * N::F32);
+      for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf, cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
-      }
+        for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf[kb], cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const int64_t row = tile * 32 + mt * 16 + li;
-        if (g == 0) {  // pos_out[:, 0] is the density: its gradient is dL/dsigma through the ReLU
-          const float ds = (a.d_sigma && row < a.M && dens[mt]) ? a.d_sigma[row] * s : 0.0f;
-          acc[mt][0] = ds;
-        }
+        // pos_out[:, 0] is the density: its gradient is dL/dsigma through the ReLU
+        const float dsv = dens[mt] ? cur[mt].ds * s : 0.0f;
+        acc[mt][0] = g == 0 ? dsv : acc[mt][0];
         dpo[mt] = to_h4(acc[mt]);
-        st4(Gfree, LH, mt * 16 + li, 4 * g, dpo[mt]);
+        st4g(Gfree, LH, mt * 16 + li, 4 * g, dpo[mt]);
       }
     }
-    wave_sync();
+    STAMP(4);
     // ---- pos output layer: dW_P1 (16 x W) += dpo^T · X_ph ; dhp = P1^T dpo
+    h4 dhp[2][NT];
     {
       const h8 ga = tr_read(Gfree, LH, 0, lane);
+      h8 xp[NT];
+      h4 wf[NT], mk[2][NT];
 #pragma unroll
-      for (int kt = 0; kt < NT; ++kt) dP1[kt] = mma32(ga, tr_read(Xph, LH, 16 * kt, lane), dP1[kt]);
-    }
-    h4 dhp[2][NT];
+      for (int kt = 0; kt < NT; ++kt) {
+        xp[kt] = tr_read(Xph, LH, 16 * kt, lane);
+        wf[kt] = bfrag16(N::oBP1 + kt * N::F16);
 #pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
-      const h4 wf = bfrag16(N::oBP1 + kt * N::F16);
+        for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xph, LH, mt * 16 + li, 16 * kt + 4 * g);
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        dhp[mt][kt] = mask_h4(mma16(wf, dpo[mt], z4), t[mt].hp[kt]);
-        st4(Gdh0, LH, mt * 16 + li, 16 * kt + 4 * g, dhp[mt][kt]);
+      for (int kt = 0; kt < NT; ++kt) mma32_acc(dP1[kt], ga, xp[kt]);
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          dhp[mt][kt] = mask_h4(mma16(wf[kt], dpo[mt], z4), mk[mt][kt]);
+          st4g(Gdh0, LH, mt * 16 + li, 16 * kt + 4 * g, dhp[mt][kt]);
+        }
       }
     }
-    wave_sync();
+    STAMP(5);
     // ---- pos input layer: dW_P0 (W x 32) += dhp^T · X_pe ; d_enc = P0^T dhp
     {
       const h8 x0 = tr_read(Xpe, LX, 0, lane), x1 = tr_read(Xpe, LX, 16, lane);
+      h8 gp[NT], wf[2 * KB];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) gp[nt] = tr_read(Gdh0, LH, 16 * nt, lane);
+#pragma unroll
+      for (int i = 0; i < 2 * KB; ++i) wf[i] = bfrag32(N::oBP0 + i * N::F32);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const h8 ga = tr_read(Gdh0, LH, 16 * nt, lane);
-        dP0[nt * 2] = mma32(ga, x0, dP0[nt * 2]);
-        dP0[nt * 2 + 1] = mma32(ga, x1, dP0[nt * 2 + 1]);
-      }
-    }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      f4 acc[2] = {z4, z4};
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        const h8 wf = bfrag32(N::oBP0 + (kt * KB + kb) * N::F32);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf, cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
+        mma32_acc(dP0[nt * 2], gp[nt], x0);
+        mma32_acc(dP0[nt * 2 + 1], gp[nt], x1);
       }
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int64_t row = tile * 32 + mt * 16 + li;
-        if (row < a.M) {
-          const f4 v = acc[mt] * inv_s;
-          *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
+      for (int kt = 0; kt < 2; ++kt) {
+        f4 acc[2] = {z4, z4};
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf[kt * KB + kb], cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int64_t row = tile * 32 + mt * 16 + li;
+          if (full || row < a.M) {
+            const f4 v = acc[mt] * inv_s;
+            *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
+          }
         }
       }
     }
-    wave_sync();
-  }
+    STAMP(6);
+  };
+  for (int64_t tile = t_begin; tile < t_full_end; ++tile) process(std::integral_constant<bool, true>{}, tile);
+  for (int64_t tile = t_full_end > t_begin ? t_full_end : t_begin; tile < t_end; ++tile)
+    process(std::integral_constant<bool, false>{}, tile);
 
+#ifdef FIELD_STAMP
+  if (stamp_on && lane == 0) {
+    for (int k = 0; k < 8; ++k) g_stamp[k] = st_acc[k];
+    g_stamp[8] = static_cast<unsigned long long>(t_end - t_begin);
+  }
+#endif
+  agpr_fence();
   // ---- flush: lane holds dW[n = 16·ntile + 4g + i][k = 16·ktile + li]
   auto flush = [&](float* dst, int ld, const f4& d, int n0, int k) {
 #pragma unroll
@@ -589,33 +877,60 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target) {
 // ---------------------------------------------------------------------------------
 static int g_target_log2 = 6;  // f16 gradient scale: max |dL/dout| of a wavefront -> 2^6
 
+// scratch for the per-wavefront gradient maxima of the backward (grown on demand)
+static float* g_wmax = nullptr;
+static int64_t g_wmax_n = 0;
+
 template <int W, int NHD>
 static int run(int op, const Args& a, hipStream_t st) {
   using N = Net<W, NHD>;
   const int waves = 4;
-  const int64_t tile_rows = op == 1 ? 16 : 32;
-  const int64_t tiles = (a.M + tile_rows - 1) / tile_rows;
-  const void* fn = op == 1 ? reinterpret_cast<const void*>(&fwd_kernel<W, NHD>)
-                           : reinterpret_cast<const void*>(&bwd_kernel<W, NHD>);
-  const size_t lds = op == 1 ? 0 : (static_cast<size_t>(N::n_bwd) + waves * N::wave_lds) * 2;
+  if (op == 1) {
+    const int64_t tiles = (a.M + 15) / 16;
+    const void* fn = reinterpret_cast<const void*>(&fwd_kernel<W, NHD>);
+    static int pc = 0;
+    if (pc == 0) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
+      pc = nb;
+    }
+    int64_t blocks = (tiles + waves - 1) / waves;
+    if (blocks > 256LL * pc) blocks = 256LL * pc;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((fwd_kernel<W, NHD>), dim3(blocks), dim3(64 * waves), 0, st, a);
+    return 0;
+  }
+  const bool fast = a.n_out == 4 && (a.d_color_stride & 3) == 0 && a.d_sigma != nullptr;
+  const size_t lds = (static_cast<size_t>(N::n_packed) + waves * N::wave_lds) * 2;  // static
   if (lds > 160 * 1024) return 1;
-  if (lds) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-  static int per_cu[3] = {0, 0, 0};
-  int& pc = per_cu[op];
+  const void* fn = fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true>)
+                        : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false>);
+  static int pc = 0;
   if (pc == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * waves, lds) != hipSuccess || nb < 1) nb = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
     pc = nb;
   }
+  const int64_t tiles = (a.M + 31) / 32;
+  // one resident wavefront per slot, each owning a contiguous range of tiles
   int64_t blocks = (tiles + waves - 1) / waves;
-  const int64_t cap = 256LL * pc;  // persistent: one resident wave per slot
-  if (blocks > cap) blocks = cap;
+  if (blocks > 256LL * pc) blocks = 256LL * pc;
   if (blocks < 1) blocks = 1;
-  if (op == 1)
-    hipLaunchKernelGGL((fwd_kernel<W, NHD>), dim3(blocks), dim3(64 * waves), 0, st, a);
+  const int64_t nw = blocks * waves;
+  const int64_t tpw = (tiles + nw - 1) / nw;
+  if (g_wmax_n < nw) {
+    if (g_wmax) (void)hipFree(g_wmax);
+    g_wmax = nullptr;
+    g_wmax_n = 0;
+    if (hipMalloc(&g_wmax, nw * sizeof(float)) != hipSuccess) return 2;
+    g_wmax_n = nw;
+  }
+  hipLaunchKernelGGL(absmax_kernel, dim3(nw), dim3(256), 0, st, a, tpw * 32, g_wmax);
+  const float target = ldexpf(1.0f, g_target_log2);
+  if (fast)
+    hipLaunchKernelGGL((bwd_kernel<W, NHD, true>), dim3(blocks), dim3(64 * waves), 0, st, a, target, tpw, g_wmax);
   else
-    hipLaunchKernelGGL((bwd_kernel<W, NHD>), dim3(blocks), dim3(64 * waves), lds, st, a,
-                       ldexpf(1.0f, g_target_log2));
+    hipLaunchKernelGGL((bwd_kernel<W, NHD, false>), dim3(blocks), dim3(64 * waves), 0, st, a, target, tpw, g_wmax);
   return 0;
 }
 
@@ -760,8 +1075,15 @@ extern "C" int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* d
   a.d_enc_stride = d_enc_stride;
   a.g_pos = g_pos;
   a.g_dir = g_dir;
-  ANR_CHECK_ARG(dispatch(v, 2, a, reinterpret_cast<hipStream_t>(stream)) == 0,
-                "anr_ingp_field_bwd: no kernel for this shape");
+  const int rc = dispatch(v, 2, a, reinterpret_cast<hipStream_t>(stream));
+  ANR_CHECK_ARG(rc != 2, "anr_ingp_field_bwd: scratch allocation failed");
+  ANR_CHECK_ARG(rc == 0, "anr_ingp_field_bwd: no kernel for this shape");
   ANR_CHECK_LAUNCH("anr_ingp_field_bwd");
   return ANR_OK;
 }
+
+#ifdef FIELD_STAMP
+extern "C" int anr_debug_field_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(anr::field::g_stamp), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -1;
+}
+#endif

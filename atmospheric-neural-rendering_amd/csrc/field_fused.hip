@@ -32,6 +32,12 @@
 #ifndef FIELD_EXP
 #define FIELD_EXP 0
 #endif
+// Stage barrier of the backward: which instruction classes may be scheduled across the
+// point where a stage's LDS reads have been issued (sched_barrier mask: 0x1 ALU, 0x2
+// VALU, 0x4 SALU, 0x8 MFMA; memory instructions never cross).
+#ifndef FIELD_STAGE_MASK
+#define FIELD_STAGE_MASK 0
+#endif
 
 namespace anr {
 namespace field {
@@ -662,7 +668,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       // all forward fragments in flight at once, then the five layers
       FwdWeights<W, NHD> fwl;
       fwl.load(wbt, lane);
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
       tile_forward<W, NHD, 2>(fwl, cur, valid, g, t, Sink{Xpe, Xde, Xph, Xd0, Xd1, li, g});
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
@@ -691,7 +697,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xlast, LH, mt * 16 + li, 16 * kt + 4 * g);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) mma32_acc(dD2[kt], ga, xl[kt]);
 #pragma unroll
@@ -719,7 +725,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xd0, LH, mt * 16 + li, 16 * kt + 4 * g);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -755,7 +761,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       for (int nt = 0; nt < NT; ++nt) gd[nt] = tr_read(Gdh0, LH, 16 * nt, lane);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) wf[kb] = bfrag32(N::oBD0 + kb * N::F32);
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         mma32_acc(dD0[nt * 2], gd[nt], x0);
@@ -789,7 +795,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xph, LH, mt * 16 + li, 16 * kt + 4 * g);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) mma32_acc(dP1[kt], ga, xp[kt]);
 #pragma unroll
@@ -810,7 +816,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       for (int nt = 0; nt < NT; ++nt) gp[nt] = tr_read(Gdh0, LH, 16 * nt, lane);
 #pragma unroll
       for (int i = 0; i < 2 * KB; ++i) wf[i] = bfrag32(N::oBP0 + i * N::F32);
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         mma32_acc(dP0[nt * 2], gp[nt], x0);

@@ -22,6 +22,11 @@
 
 #include "anr_common.h"
 
+// Profiling ablation (tools): 1 = backward without its atomics. 0 in product builds.
+#ifndef HASH_EXP
+#define HASH_EXP 0
+#endif
+
 #include <cmath>
 #include <cstdlib>
 
@@ -47,8 +52,12 @@ __device__ __forceinline__ uint32_t grid_index(uint32_t T, uint32_t res, const u
     index = 0;
 #pragma unroll
     for (int d = 0; d < D; ++d) index ^= g[d] * primes[d];
+    // hashed levels have T = 2^log2_hashmap_size (checked by make_levels): % T == & (T-1)
+    return index & (T - 1u);
   }
-  return index % T;
+  // dense levels: index < T except at the far faces (a corner at res) or for coordinates
+  // outside [0, 1]; the division is only paid there
+  return index < T ? index : index % T;
 }
 
 template <typename T, int F>
@@ -425,7 +434,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           if (map[c] < 0) {
-            if (acc[c] != 0.0f)
+            if (acc[c] != 0.0f && (HASH_EXP & 1) == 0)
               atomicAdd(grad + static_cast<int64_t>(corner_index<D>(cell, b, c, T, res)) * 2,
                         acc[c]);
           } else {
@@ -467,12 +476,23 @@ static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
     G->res[l] = d->resolutions[l];
     G->scale[l] = d->scales[l];
     if (G->size[l] == 0) return false;
+    // grid_index: a level too large for a dense table is hashed, and its size must be a
+    // power of two there (always true for tcnn's min(next_mult(res^D, 8), 2^log2T))
+    uint64_t dense = 1;
+    for (int k = 0; k < d->n_dims && dense <= G->size[l]; ++k) dense *= G->res[l];
+    if (dense > G->size[l] && (G->size[l] & (G->size[l] - 1)) != 0) return false;
   }
   return true;
 }
 
 // v2: one chunk per wave; aim for >= 32K waves (8 per SIMD on 1024 SIMDs, x4 slack).
+static int64_t env_k(const char* name) {
+  const char* e = getenv(name);  // profiling override of the chunk length
+  return e ? atoll(e) : 0;
+}
 static int64_t pick_chunk_v2(int64_t M) {
+  static const int64_t over = env_k("ANR_HASH_KB");
+  if (over > 0) return over;
   int64_t K = M / 32768;
   if (K < 1) K = 1;
   if (K > 128) K = 128;
@@ -492,6 +512,8 @@ static bool bwd_v2() { return g_hashgrid_mode != 1; }
 // Samples per chunk: long chunks amortise the per-cell gathers/atomics, but the grid
 // must still fill 256 CUs. Aim for >= 64K chunks.
 static int64_t pick_chunk(int64_t M) {
+  static const int64_t over = env_k("ANR_HASH_KF");
+  if (over > 0) return over;
   int64_t K = M / 65536;
   if (K < 1) K = 1;
   if (K > 64) K = 64;

@@ -11,7 +11,8 @@ Data parallel over rays, one process per GPU, weak scaling (8192 rays per rank).
 
 Rank 0 prints ONE JSON line. ``roofline`` is for the kernel that takes the most time per
 step, timed with HIP events on the launch stream inside the timed region; its
-algorithmic bytes per sample are defined in DESIGN.md. ``cpu_baseline`` times the
+algorithmic bytes / FLOPs per launch (kernel_models) are compulsory
+HBM traffic and dense MFMA work, and the bound is whichever fraction of peak is larger. ``cpu_baseline`` times the
 oracle's CPU restatement of the configs/nerf.json train step (rank 0, N = 1 only).
 """
 
@@ -33,23 +34,35 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_F16_PEAK_TF = 2500.0  # dense fp16/bf16 MFMA (spec, no sparsity)
 
-# Algorithmic work per unit. Hash grid, L=16 levels, F=2, D=3:
-#   fwd: 12 B coords + 16*8*2*2 B f16 corner features + 32*2 B f16 output = 588 B/sample
-#   bwd: 12 B coords + 32*4 B f32 dL/dfeature + 16*8*2*4 B f32 gradient read+write
-#        (read-modify-write) = 12 + 128 + 2048 = 2188 B/sample
-UNIT_BYTES = {"hash_fwd": 588.0, "hash_bwd": 2188.0}
 
+def kernel_models(pipe, M: int) -> dict:
+    """Algorithmic work per launch of each hot kernel.
 
-def mlp_flops_per_sample(pipe) -> dict:
-    def f(desc):
-        dims = ([desc.n_input_padded] + [desc.width] * desc.n_hidden_layers
-                + [desc.n_output_padded])
+    bytes = compulsory HBM traffic: every per-sample stream read or written once, every
+    table/weight read (or read-modify-written) once per launch; gathers and atomics that
+    the L2/MALL absorb are not counted. flops = dense MFMA work at the padded widths.
+    """
+    grid = pipe.pos_encoder.hash_grids[0]
+    n_table = grid.desc.n_params                # f16 table entries x features
+    pos, dirm = pipe.pos_mlp.desc, pipe.dir_mlp.desc
+
+    def mlp_flops(d):
+        dims = [d.n_input_padded] + [d.width] * d.n_hidden_layers + [d.n_output_padded]
         return 2.0 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
-    pos, dirm = f(pipe.pos_mlp.desc), f(pipe.dir_mlp.desc)
-    # fwd = 1x; bwd = recompute fwd + dIn + dW = 3x
-    return {"pos_mlp_fwd": pos, "dir_mlp_fwd": dirm, "pos_mlp_bwd": 3 * pos,
-            "dir_mlp_bwd": 3 * dirm}
 
+    f_fwd = mlp_flops(pos) + mlp_flops(dirm)
+    nb = dirm.n_output
+    enc_b = 2 * grid.n_out                      # f16 features
+    return {
+        # coords in, features out; table read once
+        "hash_fwd": {"bytes": M * (12 + enc_b) + 2 * n_table, "flops": 0.0},
+        # coords + f32 dL/denc in; f32 table gradient read-modify-written once
+        "hash_bwd": {"bytes": M * (12 + 4 * grid.n_out) + 8 * n_table, "flops": 0.0},
+        # enc in, sigma + color out
+        "field_fwd": {"bytes": M * (enc_b + 4 + 4 * nb), "flops": M * f_fwd},
+        # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; forward recompute + dX + dW
+        "field_bwd": {"bytes": M * (enc_b + 4 * nb + 4 + 4 * grid.n_out), "flops": 3 * M * f_fwd},
+    }
 
 def ingp_config(variant: str, n_samples: int) -> dict:
     import __graft_entry__ as ge
@@ -164,28 +177,32 @@ def main():
     kernels, roofline = {}, None
     if timer:
         summ = timer.summary()
-        flops = mlp_flops_per_sample(pipe)
         M = args.batch * args.samples
-        for name, s in sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"]):
-            entry = {"avg_ms": round(s["avg_ms"], 4),
-                     "ms_per_step": round(s["total_ms"] / args.steps, 4)}
-            if name in UNIT_BYTES:
-                gbs = UNIT_BYTES[name] * M / (s["avg_ms"] * 1e-3) / 1e9
-                entry.update(bound="hbm", achieved=round(gbs, 1),
-                             frac=round(gbs / HBM_PEAK_GBS, 4))
-            elif name in flops:
-                tf = flops[name] * M / (s["avg_ms"] * 1e-3) / 1e12
-                entry.update(bound="mfma", achieved=round(tf, 2),
-                             frac=round(tf / MFMA_F16_PEAK_TF, 4))
+        models = kernel_models(pipe, M)
+        for name, st in sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"]):
+            entry = {"avg_ms": round(st["avg_ms"], 4),
+                     "ms_per_step": round(st["total_ms"] / args.steps, 4)}
+            mdl = models.get(name)
+            if mdl:
+                sec = st["avg_ms"] * 1e-3
+                gbs = mdl["bytes"] / sec / 1e9
+                tfs = mdl["flops"] / sec / 1e12
+                fb, ff = gbs / HBM_PEAK_GBS, tfs / MFMA_F16_PEAK_TF
+                entry.update(hbm_gbs=round(gbs, 1), hbm_frac=round(fb, 4),
+                             mfma_tfs=round(tfs, 2), mfma_frac=round(ff, 4),
+                             bound="hbm" if fb >= ff else "mfma")
             kernels[name] = entry
         dominant = next((n for n in kernels if "bound" in kernels[n]), None)
         if dominant:
-            k = kernels[dominant]
-            roofline = {"kernel": dominant, "bound": k["bound"], "achieved": k["achieved"],
-                        "peak": HBM_PEAK_GBS if k["bound"] == "hbm" else MFMA_F16_PEAK_TF,
-                        "unit": "GB/s" if k["bound"] == "hbm" else "TFLOP/s",
-                        "frac": k["frac"], "traffic": None,
-                        "avg_ms": k["avg_ms"], "units_per_launch": M}
+            k, mdl = kernels[dominant], models[dominant]
+            hbm = k["bound"] == "hbm"
+            roofline = {"kernel": dominant, "bound": k["bound"],
+                        "achieved": k["hbm_gbs"] if hbm else k["mfma_tfs"],
+                        "peak": HBM_PEAK_GBS if hbm else MFMA_F16_PEAK_TF,
+                        "unit": "GB/s" if hbm else "TFLOP/s",
+                        "frac": k["hbm_frac"] if hbm else k["mfma_frac"],
+                        "traffic": None, "avg_ms": k["avg_ms"], "units_per_launch": M,
+                        "algorithmic_bytes": mdl["bytes"], "algorithmic_flops": mdl["flops"]}
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc):
                 try:

@@ -27,10 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAGS = {
     "hash_fwd": "hashgrid_fwd_kernel<3, 2, __half, __half>",
     "hash_bwd": "hashgrid_bwd_v2_kernel<3, float>",
-    "dir_mlp_bwd": "bwd_kernelIDF16_Li64ELi32ELi16ELi2E",
-    "pos_mlp_bwd": "bwd_kernelIDF16_Li64ELi32ELi16ELi1E",
-    "dir_mlp_fwd": "fwd_kernelIDF16_Li64ELi32ELi16ELi2E",
-    "pos_mlp_fwd": "fwd_kernelIDF16_Li64ELi32ELi16ELi1E",
+    "field_fwd": "field::fwd_kernel<64, 2>",
+    "field_bwd": "field::bwd_kernel<64, 2, true>",
     "composite_fwd": "rb::fwd_kernel<float, 16, 1>",
     "composite_bwd": "rb::bwd_kernel<float, 16, 1>",
     "sampler": "sample_uniform_bins_kernel",

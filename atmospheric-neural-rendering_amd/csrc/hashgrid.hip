@@ -27,7 +27,9 @@
 #define HASH_EXP 0
 #endif
 
+
 #include <cmath>
+#include <type_traits>
 #include <cstdlib>
 
 namespace anr {
@@ -59,6 +61,52 @@ __device__ __forceinline__ uint32_t grid_index(uint32_t T, uint32_t res, const u
   // outside [0, 1]; the division is only paid there
   return index < T ? index : index % T;
 }
+
+// Per-level corner indexing with the per-cell work hoisted: the 2^D corner indices of a
+// cell are built from 2 values per dimension (coordinate and coordinate+1, each times the
+// dense stride or the hash prime) with one 3-input add (dense) or xor (hashed) per
+// corner. Same result as grid_index for every corner, dense wrap (far faces, coordinates
+// outside [0,1]) included; branch-free apart from the rare full modulo.
+template <int D>
+struct LevelIdx {
+  uint32_t T, mul[D];
+  bool hashed;
+  __device__ void init(uint32_t T_, uint32_t res) {
+    constexpr uint32_t primes[3] = {1u, 2654435761u, 805459861u};
+    T = T_;
+    uint64_t st = 1;
+    uint32_t stride[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      stride[d] = static_cast<uint32_t>(st);
+      st *= res;
+    }
+    hashed = st > T;  // res^D > T, as grid_index decides
+#pragma unroll
+    for (int d = 0; d < D; ++d) mul[d] = hashed ? primes[d] : stride[d];
+  }
+  // comp[d][o] = (cell[d] + o) * mul[d]  (uint32 wrap, as tcnn)
+  __device__ void dims(const uint32_t* cell, uint32_t (*comp)[2]) const {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      comp[d][0] = cell[d] * mul[d];
+      comp[d][1] = comp[d][0] + mul[d];
+    }
+  }
+  // corner c: bit d = offset along dimension d
+  __device__ uint32_t corner(const uint32_t (*comp)[2], int c) const {
+    uint32_t hx = 0u, sum = 0u;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      hx ^= comp[d][(c >> d) & 1];
+      sum += comp[d][(c >> d) & 1];
+    }
+    if (hashed) return hx & (T - 1u);
+    if (sum < T) return sum;
+    const uint32_t s1 = sum - T;
+    return s1 < T ? s1 : sum % T;
+  }
+};
 
 template <typename T, int F>
 struct Vec;
@@ -108,15 +156,23 @@ __device__ __forceinline__ void store_feat<__half, 2>(__half* p, const float* v)
   *reinterpret_cast<__half2*>(p) = __floats2half2_rn(v[0], v[1]);
 }
 
-// lanes_per_chunk (16 or 32) lanes serve one chunk; lane l within the group = level l.
+// A wavefront serves lpw consecutive levels (lane % lpw) of 64/lpw chunks (lane / lpw);
+// wavefronts cycle through the n_groups level groups of a block of chunks. Grouping few
+// levels per wave keeps the divergent gather path to the waves whose levels actually
+// change cell (fine levels: often; coarse levels: almost never).
 template <int D, int F, typename TT, typename TO>
 __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
-    GridLevels G, int n_levels, int lanes_per_chunk, const float* __restrict__ x,
+    GridLevels G, int n_levels, int lpw, int n_groups, const float* __restrict__ x,
     int64_t x_stride, int64_t M, int64_t K, const TT* __restrict__ table,
     TO* __restrict__ out, int64_t out_stride) {
-  const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int64_t chunk = gtid / lanes_per_chunk;
-  const int level = static_cast<int>(gtid % lanes_per_chunk);
+  // level group = block index mod n_groups: consecutive blocks go to different XCDs
+  // (round-robin dispatch), so with n_groups = 8 each XCD's L2 serves the table slice of
+  // its own levels only (speed only; any block placement gives the same result)
+  const int lane = static_cast<int>(threadIdx.x & 63);
+  const int lg = static_cast<int>(blockIdx.x % n_groups);
+  const int64_t wave_in = (static_cast<int64_t>(blockIdx.x / n_groups) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t chunk = wave_in * (64 / lpw) + lane / lpw;
+  const int level = lg * lpw + lane % lpw;
   const int64_t m0 = chunk * K;
   if (level >= n_levels || m0 >= M) return;
   const int64_t m1 = m0 + K < M ? m0 + K : M;
@@ -125,6 +181,8 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
   const uint32_t res = G.res[level];
   const uint32_t T = G.size[level];
   const TT* __restrict__ grid = table + static_cast<int64_t>(G.offset[level]) * F;
+  LevelIdx<D> li;
+  li.init(T, res);
 
   uint32_t cell[D];
   bool have = false;
@@ -146,14 +204,11 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
     }
     if (!same) {
       have = true;
+      uint32_t comp[D][2];
+      li.dims(g, comp);
 #pragma unroll
-      for (int c = 0; c < (1 << D); ++c) {
-        uint32_t gc[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) gc[d] = g[d] + ((c >> d) & 1);
-        const uint32_t idx = grid_index<D>(T, res, gc);
-        Vec<TT, F>::load(grid + static_cast<int64_t>(idx) * F, val[c]);
-      }
+      for (int c = 0; c < (1 << D); ++c)
+        Vec<TT, F>::load(grid + static_cast<int64_t>(li.corner(comp, c)) * F, val[c]);
 #pragma unroll
       for (int d = 0; d < D; ++d) cell[d] = g[d];
     }
@@ -168,7 +223,8 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
 #pragma unroll
       for (int f = 0; f < F; ++f) acc[f] = fmaf(wt, val[c][f], acc[f]);
     }
-    store_feat<TO, F>(out + m * out_stride + level * F, acc);
+    if constexpr ((HASH_EXP & 2) == 0) store_feat<TO, F>(out + m * out_stride + level * F, acc);
+    else if (acc[0] == 12345.0f) out[0] = from_f32<TO>(acc[F - 1]);  // keep the work alive
   }
 }
 
@@ -403,6 +459,8 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
   const uint32_t res = G.res[level];
   const uint32_t T = G.size[level];
   float* __restrict__ grad = dtable + static_cast<int64_t>(G.offset[level]) * 2 + f;
+  LevelIdx<D> li;
+  li.init(T, res);
 
   uint32_t cell[D];
   bool have = false;
@@ -412,13 +470,13 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
 #pragma unroll
   for (int c = 0; c < NC; ++c) acc[c] = 0.0f;
 
-  for (int64_t m = m0; m < m1; ++m) {
+  auto step = [&](const float* xv, float gv) {
     float w[D];
     uint32_t g[D];
     bool same = have;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const float p = fmaf(scale, x[m * x_stride + d], 0.5f);
+      const float p = fmaf(scale, xv[d], 0.5f);
       const float fl = floorf(p);
       g[d] = static_cast<uint32_t>(static_cast<int>(fl));
       w[d] = p - fl;
@@ -429,14 +487,15 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
         int map[NC];
         corner_shift<D>(cell, g, g[0] == cell[0], map);
         float nacc[NC];
+        uint32_t comp[D][2];
+        li.dims(cell, comp);
 #pragma unroll
         for (int c = 0; c < NC; ++c) nacc[c] = 0.0f;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           if (map[c] < 0) {
             if (acc[c] != 0.0f && (HASH_EXP & 1) == 0)
-              atomicAdd(grad + static_cast<int64_t>(corner_index<D>(cell, b, c, T, res)) * 2,
-                        acc[c]);
+              atomicAdd(grad + static_cast<int64_t>(li.corner(comp, b | (c << 1))) * 2, acc[c]);
           } else {
 #pragma unroll
             for (int c2 = 0; c2 < NC; ++c2)
@@ -450,7 +509,6 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
       for (int d = 0; d < D; ++d) cell[d] = g[d];
       have = true;
     }
-    const float gv = to_f32<TG>(dout[m * dout_stride + level * 2 + f]);
     const float wx = b ? w[0] : 1.0f - w[0];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -459,12 +517,42 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
       for (int d = 1; d < D; ++d) wt *= Corners<D>::bit(c, d) ? w[d] : 1.0f - w[d];
       acc[c] = fmaf(wt, gv, acc[c]);
     }
+  };
+
+  // Batches of BS samples: the next batch's coordinates and gradients are loaded while
+  // this one is processed (indices clamped to the chunk, so the loads need no branch).
+  constexpr int BS = 8;
+  float xb[BS][D], xn[BS][D];
+  TG gb[BS], gn[BS];
+  auto load_batch = [&](int64_t mb, float (*xo)[D], TG* go) {
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      const int64_t m = mb + j < m1 ? mb + j : m1 - 1;
+#pragma unroll
+      for (int d = 0; d < D; ++d) xo[j][d] = x[m * x_stride + d];
+      go[j] = dout[m * dout_stride + level * 2 + f];
+    }
+  };
+  load_batch(m0, xb, gb);
+  for (int64_t mb = m0; mb < m1; mb += BS) {
+    load_batch(mb + BS, xn, gn);
+#pragma unroll
+    for (int j = 0; j < BS; ++j)
+      if (mb + j < m1) step(xb[j], to_f32<TG>(gb[j]));
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      gb[j] = gn[j];
+#pragma unroll
+      for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
+    }
   }
   if (have) {
+    uint32_t comp[D][2];
+    li.dims(cell, comp);
 #pragma unroll
     for (int c = 0; c < NC; ++c)
       if (acc[c] != 0.0f)
-        atomicAdd(grad + static_cast<int64_t>(corner_index<D>(cell, b, c, T, res)) * 2, acc[c]);
+        atomicAdd(grad + static_cast<int64_t>(li.corner(comp, b | (c << 1))) * 2, acc[c]);
   }
 }
 
@@ -509,6 +597,16 @@ static int g_hashgrid_mode = [] {
 static bool fwd_v2() { return g_hashgrid_mode == 2; }
 static bool bwd_v2() { return g_hashgrid_mode != 1; }
 
+// Levels per wavefront of the forward walker (1, 2, 4, 8, 16, 32 or 64).
+static int fwd_lpw() {
+  static const int v = [] {
+    const char* e = getenv("ANR_HASH_LPW");  // profiling override
+    const int k = e ? atoi(e) : 0;
+    return (k >= 1 && k <= 64 && (64 % k) == 0) ? k : 16;
+  }();
+  return v;
+}
+
 // Samples per chunk: long chunks amortise the per-cell gathers/atomics, but the grid
 // must still fill 256 CUs. Aim for >= 64K chunks.
 static int64_t pick_chunk(int64_t M) {
@@ -540,15 +638,16 @@ static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
     ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v2)");
     return ANR_OK;
   }
-  const int lpc = d->n_levels <= 16 ? 16 : 32;
+  const int lpw = fwd_lpw();
+  const int n_groups = static_cast<int>(ceil_div(d->n_levels, lpw));
   const int64_t K = pick_chunk(M);
   const int64_t chunks = ceil_div(M, K);
-  const int64_t threads = chunks * lpc;
-  const dim3 grid(static_cast<unsigned>(ceil_div(threads, 256))), block(256);
+  const int64_t blocks_per_group = ceil_div(ceil_div(chunks, 64 / lpw), 4);
+  const dim3 grid(static_cast<unsigned>(blocks_per_group * n_groups)), block(256);
 #define ANR_HG_FWD(TT, TO)                                                                  \
   hipLaunchKernelGGL((hashgrid_fwd_kernel<D, F, TT, TO>), grid, block, 0, s, G,             \
-                     d->n_levels, lpc, x, x_stride, M, K, static_cast<const TT*>(table),    \
-                     static_cast<TO*>(out), out_stride)
+                     d->n_levels, lpw, n_groups, x, x_stride, M, K,                          \
+                     static_cast<const TT*>(table), static_cast<TO*>(out), out_stride)
   if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD(__half, __half);
   else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD(__half, float);
   else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD(float, __half);

@@ -93,6 +93,12 @@ class MlpDesc(Structure):
 
 
 # name -> (restype, argtypes). Mirrors include/anr.h one to one.
+class PosencDesc(Structure):
+    """anr_posenc_desc (include/anr.h)."""
+
+    _fields_ = [("n_dims", c_int32), ("interleaved", c_int32), ("L", c_int32 * 8)]
+
+
 _P = c_void_p
 _SIGNATURES = {
     "anr_abi_version": (c_int32, []),
@@ -102,6 +108,20 @@ _SIGNATURES = {
         [_P, _P, _P, _P, _P, c_int64, c_int32, _P, _P, POINTER(PrepParams), _P, _P],
     ),
     "anr_preprocess_points": (c_int32, [_P, c_int64, POINTER(PrepParams), _P, _P]),
+    "anr_preprocess_points_bwd": (c_int32, [_P, c_int64, POINTER(PrepParams), _P, _P, _P]),
+    "anr_posenc_width": (c_int32, [POINTER(PosencDesc)]),
+    "anr_posenc_fwd": (c_int32, [POINTER(PosencDesc), _P, c_int64, c_int64, _P, c_int64, _P]),
+    "anr_posenc_bwd": (c_int32, [POINTER(PosencDesc), _P, c_int64, _P, c_int64, _P, _P]),
+    "anr_sample_pdf_fwd": (
+        c_int32,
+        [_P, c_int64, c_int32, _P, _P, _P, _P, c_int64, c_int32, c_int32, _P, _P, _P, _P, _P,
+         _P],
+    ),
+    "anr_sample_pdf_bwd": (
+        c_int32,
+        [_P, c_int64, c_int32, _P, _P, _P, _P, _P, _P, c_int64, c_int32, c_int32, _P, _P, _P,
+         _P],
+    ),
     "anr_hashgrid_init": (
         c_int32,
         [POINTER(HashGridDesc), c_int32, c_int32, c_int32, c_int32, c_float, c_int32],
@@ -285,6 +305,22 @@ def hashgrid_desc(n_dims: int, n_levels: int, n_features: int, base_resolution: 
     d = HashGridDesc()
     call("anr_hashgrid_init", ctypes.byref(d), n_dims, n_levels, n_features,
          base_resolution, per_level_scale, log2_hashmap_size)
+    return d
+
+
+def posenc_desc(L, n_dims: int = 3) -> PosencDesc:
+    """encoders.py:4-28 frequency spec: int L (interleaved) or a per-coordinate list."""
+    d = PosencDesc()
+    if isinstance(L, int):
+        d.n_dims, d.interleaved = n_dims, 1
+        d.L[0] = L
+    else:
+        L = list(L)
+        d.n_dims, d.interleaved = len(L), 0
+        for i, v in enumerate(L):
+            d.L[i] = int(v)
+    if load().anr_posenc_width(ctypes.byref(d)) < 0:
+        raise ANRError(f"unsupported positional-encoding spec {L!r}")
     return d
 
 

@@ -5,9 +5,10 @@ from __future__ import annotations
 from typing import Any
 
 from .instant_ngp import InstantNGPPipeline
+from .nerf import NeRFPipeline
 from .pipeline import Pipeline
 
-_PIPELINES: dict[str, type] = {"InstantNGP": InstantNGPPipeline}
+_PIPELINES: dict[str, type] = {"NeRF": NeRFPipeline, "InstantNGP": InstantNGPPipeline}
 
 
 def register(name: str, cls: type) -> None:

@@ -94,11 +94,82 @@ def sample_and_preprocess(
     return pts, z, coords
 
 
+class _PreprocessFn(torch.autograd.Function):
+    """harp2.py:372-386 on the GPU (K2); differentiable w.r.t. the points — the NeRF
+    pipeline back-propagates through it into the pdf samples."""
+
+    @staticmethod
+    def forward(ctx, flat, prep):
+        out = torch.empty_like(flat)
+        call("anr_preprocess_points", ptr(flat), flat.shape[0], prep, ptr(out),
+             _lib.stream(flat.device))
+        ctx.save_for_backward(flat)
+        ctx.prep = prep
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        (flat,) = ctx.saved_tensors
+        d_out = d_out.float().contiguous()
+        d_in = torch.empty_like(flat)
+        call("anr_preprocess_points_bwd", ptr(flat), flat.shape[0], ctx.prep, ptr(d_out),
+             ptr(d_in), _lib.stream(flat.device))
+        return d_in, None
+
+
 def preprocess_points(pts: torch.Tensor, prep: "_lib.PrepParams") -> torch.Tensor:
-    """Apply a preprocessor to arbitrary points (..., 3) (extract path)."""
+    """Apply a preprocessor to arbitrary points (..., 3); differentiable w.r.t. pts."""
     shp = pts.shape
     flat = pts.reshape(-1, 3).float().contiguous()
-    out = torch.empty_like(flat)
-    call("anr_preprocess_points", ptr(flat), flat.shape[0], prep, ptr(out),
-         _lib.stream(pts.device))
-    return out.view(shp)
+    return _PreprocessFn.apply(flat, prep).view(shp)
+
+
+class _SamplePdfFn(torch.autograd.Function):
+    """samplers.py:50-103: one wavefront per ray (searchsorted on an f64-accumulated cdf,
+    rank sort of coarse + fine z); backward into the coarse weights through t_in_bin."""
+
+    @staticmethod
+    def forward(ctx, weights, z_c, u, origin, direction, n_samples):
+        B, Nc = z_c.shape
+        dev = z_c.device
+        Nt = Nc + n_samples
+        w = weights.float().contiguous()
+        z = torch.empty(B, Nt, device=dev)
+        pts = torch.empty(B, Nt, 3, device=dev)
+        src = torch.empty(B, Nt, device=dev, dtype=torch.int32)
+        inds = torch.empty(B, n_samples, device=dev, dtype=torch.int32)
+        cdf = torch.empty(B, Nc - 1, device=dev)
+        call("anr_sample_pdf_fwd", ptr(w), w.stride(0), w.stride(1), ptr(z_c), ptr(u),
+             ptr(origin), ptr(direction), B, Nc, n_samples, ptr(z), ptr(pts), ptr(src),
+             ptr(inds), ptr(cdf), _lib.stream(dev))
+        ctx.save_for_backward(w, z_c, u, direction, src, inds, cdf)
+        ctx.n_samples = n_samples
+        return pts, z
+
+    @staticmethod
+    def backward(ctx, d_pts, d_z):
+        w, z_c, u, direction, src, inds, cdf = ctx.saved_tensors
+        B, Nc = z_c.shape
+        d_w = torch.zeros_like(w)
+        d_pts = d_pts.float().contiguous() if d_pts is not None else None
+        d_z = d_z.float().contiguous() if d_z is not None else None
+        call("anr_sample_pdf_bwd", ptr(w), w.stride(0), w.stride(1), ptr(z_c), ptr(u),
+             ptr(direction), ptr(src), ptr(inds), ptr(cdf), B, Nc, ctx.n_samples, ptr(d_z),
+             ptr(d_pts), ptr(d_w), _lib.stream(w.device))
+        return d_w, None, None, None, None, None
+
+
+def sample_pdf(ray_batch: Mapping[str, torch.Tensor], pdf_discrete: torch.Tensor,
+               z_vals_c: torch.Tensor, n_samples: int = 128, u: torch.Tensor | None = None
+               ) -> tuple[torch.Tensor, torch.Tensor]:
+    """samplers.py:50-103. pdf_discrete (B, Nc, S) — channel 0 is the pdf (the render
+    weights); u (B, n_samples) overrides the torch.rand draws. Returns pts (B, Nc+n, 3) and
+    sorted z (B, Nc+n); gradients reach pdf_discrete as in the reference."""
+    origin = ray_batch["origin"].float().contiguous()
+    direction = ray_batch["dir"].float().contiguous()
+    B, Nc = z_vals_c.shape
+    if u is None:
+        u = torch.rand(B, n_samples, device=z_vals_c.device)
+    u = u.float().contiguous()
+    return _SamplePdfFn.apply(pdf_discrete, z_vals_c.float().contiguous(), u, origin,
+                              direction, n_samples)

@@ -44,6 +44,8 @@ __device__ __forceinline__ double py_mod(double a, double b) {
 __device__ __forceinline__ float clip1(float v) { return v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v); }
 
 // preprocess_coords for one point p (normalized scene frame, f32) -> coords (f32).
+// kClip=false stops before clip(-1, 1) (the backward's clamp mask needs the raw value).
+template <bool kClip = true>
 __device__ __forceinline__ void preprocess_point(const PrepDev& P, float px, float py,
                                                  float pz, float* out) {
   float cx = px, cy = py, cz = pz;
@@ -69,9 +71,14 @@ __device__ __forceinline__ void preprocess_point(const PrepDev& P, float px, flo
     const double b = 2.0 * (lon_d - P.lon_min) / P.lon_range - 1.0;
     const double c = 2.0 * alt / P.h - 1.0;
     // .to(float32) then clip(-1, 1), harp2.py:384-385
-    cx = clip1(static_cast<float>(a));
-    cy = clip1(static_cast<float>(b));
-    cz = clip1(static_cast<float>(c));
+    cx = static_cast<float>(a);
+    cy = static_cast<float>(b);
+    cz = static_cast<float>(c);
+    if (kClip) {
+      cx = clip1(cx);
+      cy = clip1(cy);
+      cz = clip1(cz);
+    }
   }
   if (P.ngp_remap) {
     // pts = (pts + 1) / 2 ; pts[..., 2] /= alt_compress_factor (instant_ngp.py:149,160)
@@ -83,6 +90,100 @@ __device__ __forceinline__ void preprocess_point(const PrepDev& P, float px, flo
   out[0] = cx;
   out[1] = cy;
   out[2] = cz;
+}
+
+// ---- backward of preprocess_point (NeRF back-propagates into the sample points through
+// the fp64 preprocessor, harp2.py:372-386): forward-mode dual numbers over (px, py, pz).
+struct D3 {
+  double v, d[3];
+};
+__device__ __forceinline__ D3 dc(double v) { return D3{v, {0.0, 0.0, 0.0}}; }
+__device__ __forceinline__ D3 operator+(D3 a, D3 b) {
+  return D3{a.v + b.v, {a.d[0] + b.d[0], a.d[1] + b.d[1], a.d[2] + b.d[2]}};
+}
+__device__ __forceinline__ D3 operator-(D3 a, D3 b) {
+  return D3{a.v - b.v, {a.d[0] - b.d[0], a.d[1] - b.d[1], a.d[2] - b.d[2]}};
+}
+__device__ __forceinline__ D3 operator*(D3 a, D3 b) {
+  return D3{a.v * b.v, {a.d[0] * b.v + a.v * b.d[0], a.d[1] * b.v + a.v * b.d[1],
+                        a.d[2] * b.v + a.v * b.d[2]}};
+}
+__device__ __forceinline__ D3 operator/(D3 a, D3 b) {
+  const double q = a.v / b.v, ib = 1.0 / b.v;
+  return D3{q, {(a.d[0] - q * b.d[0]) * ib, (a.d[1] - q * b.d[1]) * ib, (a.d[2] - q * b.d[2]) * ib}};
+}
+__device__ __forceinline__ D3 scale(D3 a, double k) {
+  return D3{a.v * k, {a.d[0] * k, a.d[1] * k, a.d[2] * k}};
+}
+__device__ __forceinline__ D3 dsin(D3 a) {
+  const double c = cos(a.v);
+  return D3{sin(a.v), {c * a.d[0], c * a.d[1], c * a.d[2]}};
+}
+__device__ __forceinline__ D3 dcos(D3 a) {
+  const double s = -sin(a.v);
+  return D3{cos(a.v), {s * a.d[0], s * a.d[1], s * a.d[2]}};
+}
+__device__ __forceinline__ D3 dsqrt(D3 a) {
+  const double r = sqrt(a.v), k = 0.5 / r;
+  return D3{r, {k * a.d[0], k * a.d[1], k * a.d[2]}};
+}
+__device__ __forceinline__ D3 datan2(D3 y, D3 x) {
+  const double den = x.v * x.v + y.v * y.v;
+  D3 r{atan2(y.v, x.v), {}};
+  for (int k = 0; k < 3; ++k) r.d[k] = (x.v * y.d[k] - y.v * x.d[k]) / den;
+  return r;
+}
+
+// d out_j / d p_k of preprocess_point (values follow the forward; the f32 cast passes the
+// gradient through, clip(-1, 1) passes it where -1 <= value <= 1, as torch.clamp does).
+__device__ void preprocess_jacobian(const PrepDev& P, float px, float py, float pz,
+                                    double J[3][3]) {
+  for (int j = 0; j < 3; ++j)
+    for (int k = 0; k < 3; ++k) J[j][k] = j == k ? 1.0 : 0.0;
+  if (P.mode == 1) {
+    const double sf = static_cast<double>(P.scale_f);
+    const D3 x{static_cast<double>(px * P.scale_f) + P.offset[0], {sf, 0.0, 0.0}};
+    const D3 y{static_cast<double>(py * P.scale_f) + P.offset[1], {0.0, sf, 0.0}};
+    const D3 z{static_cast<double>(pz * P.scale_f) + P.offset[2], {0.0, 0.0, sf}};
+    const D3 lon = datan2(y, x);
+    const D3 D = dsqrt(x * x + y * y);
+    const D3 u = datan2(z / D, dc(0.0 + kA / kB));
+    const D3 su = dsin(u), cu = dcos(u);
+    const D3 lat = datan2(z + scale(su * su * su, kE2 * kB), D - scale(cu * cu * cu, kE * kA));
+    const D3 sl = dsin(lat);
+    const D3 Nr = dc(kA) / dsqrt(dc(1.0) - scale(sl * sl, kE));
+    const D3 alt = x / (dcos(lat) * dcos(lon)) - Nr;
+    const D3 o[3] = {scale(scale(lat, 180.0 / kPi), 2.0 / P.lat_range),
+                     scale(scale(lon, 180.0 / kPi), 2.0 / P.lon_range),
+                     scale(alt, 2.0 / P.h)};
+    float val[3];  // f32 values before clip and NGP remap: torch.clamp's gradient mask
+    PrepDev Q = P;
+    Q.ngp_remap = 0;
+    preprocess_point<false>(Q, px, py, pz, val);
+    for (int j = 0; j < 3; ++j) {
+      const bool pass = val[j] >= -1.0f && val[j] <= 1.0f;
+      for (int k = 0; k < 3; ++k) J[j][k] = pass ? o[j].d[k] : 0.0;
+    }
+  }
+  if (P.ngp_remap) {
+    for (int k = 0; k < 3; ++k) {
+      J[0][k] *= 0.5;
+      J[1][k] *= 0.5;
+      J[2][k] = J[2][k] * 0.5 / static_cast<double>(P.alt_compress);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) preprocess_points_bwd_kernel(
+    const float* __restrict__ pts, int64_t P_n, PrepDev P, const float* __restrict__ dcoords,
+    float* __restrict__ dpts) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= P_n) return;
+  double J[3][3];
+  preprocess_jacobian(P, pts[idx * 3 + 0], pts[idx * 3 + 1], pts[idx * 3 + 2], J);
+  const double g[3] = {dcoords[idx * 3 + 0], dcoords[idx * 3 + 1], dcoords[idx * 3 + 2]};
+  for (int k = 0; k < 3; ++k)
+    dpts[idx * 3 + k] = static_cast<float>(g[0] * J[0][k] + g[1] * J[1][k] + g[2] * J[2][k]);
 }
 
 __global__ void __launch_bounds__(256) sample_uniform_bins_kernel(
@@ -188,5 +289,18 @@ extern "C" int anr_preprocess_points(const float* pts, int64_t P_n,
   hipLaunchKernelGGL(preprocess_points_kernel, dim3(ceil_div(P_n, 256)), dim3(256), 0,
                      as_stream(stream), pts, P_n, P, coords);
   ANR_CHECK_LAUNCH("anr_preprocess_points");
+  return ANR_OK;
+}
+
+extern "C" int anr_preprocess_points_bwd(const float* pts, int64_t P, const anr_prep_params* prep,
+                                         const float* d_coords, float* d_pts,
+                                         anr_stream_t stream) {
+  ANR_CHECK_ARG(prep != nullptr && P >= 0, "anr_preprocess_points_bwd: bad arguments");
+  if (P == 0) return ANR_OK;
+  ANR_CHECK_ARG(pts && d_coords && d_pts, "anr_preprocess_points_bwd: null pointer");
+  const anr::PrepDev d = anr::make_prep(prep);
+  hipLaunchKernelGGL(anr::preprocess_points_bwd_kernel, dim3(static_cast<unsigned>((P + 255) / 256)),
+                     dim3(256), 0, reinterpret_cast<hipStream_t>(stream), pts, P, d, d_coords, d_pts);
+  ANR_CHECK_LAUNCH("anr_preprocess_points_bwd");
   return ANR_OK;
 }

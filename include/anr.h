@@ -81,6 +81,12 @@ int anr_sample_uniform_bins(const float* origin, const float* dir, const float* 
 int anr_preprocess_points(const float* pts, int64_t P, const anr_prep_params* prep,
                           float* coords, anr_stream_t stream);
 
+/* Backward of the preprocessor (the NeRF pipeline back-propagates into the sample points,
+ * harp2.py:372-386): d_pts (P,3) f32 WRITTEN = J^T d_coords, J from fp64 forward-mode
+ * derivatives of the same formula; clip passes the gradient where -1 <= value <= 1. */
+int anr_preprocess_points_bwd(const float* pts, int64_t P, const anr_prep_params* prep,
+                              const float* d_coords, float* d_pts, anr_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * K3 / K4: multi-resolution hash-grid encoding (tinycudann.Encoding otype "HashGrid",
  * instant_ngp.py:60-63,163; surface 2-D grid :78-80,173).
@@ -225,6 +231,45 @@ int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const v
                        int64_t n_per_ray, int64_t M, const float* d_sigma,
                        const float* d_color, int64_t d_color_stride, float* d_enc,
                        int64_t d_enc_stride, float* g_pos, float* g_dir, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * NeRF path (configs/nerf.json): positional encoding (encoders.py:4-28) and the
+ * hierarchical pdf sampler (samplers.py:50-103), forward and backward.
+ * ------------------------------------------------------------------------------------ */
+#define ANR_POSENC_MAX_DIMS 8
+typedef struct {
+  int32_t n_dims;       /* input coordinates per row */
+  int32_t interleaved;  /* 1: int L (per coordinate [sin f0, cos f0, sin f1, ...]),
+                           0: list L (per coordinate [sin f0..f(L-1), cos f0..f(L-1)]) */
+  int32_t L[ANR_POSENC_MAX_DIMS]; /* frequencies per coordinate (interleaved: L[0] for all) */
+} anr_posenc_desc;
+/* Output width (2 * sum of L), or -1 for a bad descriptor. */
+int32_t anr_posenc_width(const anr_posenc_desc* d);
+/* out (P, >= width) f32 row r = encoding of x row r / rows_per_x (x (P/rows_per_x, n_dims)
+ * f32); frequencies (2^l * pi) in f32 times x in f32, sinf/cosf. */
+int anr_posenc_fwd(const anr_posenc_desc* d, const float* x, int64_t rows_per_x, int64_t P,
+                   float* out, int64_t out_stride, anr_stream_t stream);
+/* dx (P, n_dims) f32 WRITTEN from dL/dout (P, >= width). */
+int anr_posenc_bwd(const anr_posenc_desc* d, const float* x, int64_t P, const float* dout,
+                   int64_t dout_stride, float* dx, anr_stream_t stream);
+/* sample_pdf forward, one wavefront per ray (3 <= Nc <= 64, 1 <= Nf <= 256).
+ *   weights: coarse render weights, element (b, j) at b*w_ray_stride + j*w_sample_stride
+ *   (channel 0 of (B, Nc, S)); z_coarse (B,Nc) f32 ascending; u (B,Nf) f32 draws.
+ *   Outputs: z (B, Nc+Nf) sorted, pts (B, Nc+Nf, 3) = o + d*z (nullable), src (B, Nc+Nf)
+ *   int32 (source of each sorted value: < Nc coarse, else Nc + sample), inds (B,Nf) int32
+ *   = searchsorted(cdf, u, right=True), cdf (B, Nc-1) f32 (saved for the backward). */
+int anr_sample_pdf_fwd(const float* weights, int64_t w_ray_stride, int32_t w_sample_stride,
+                       const float* z_coarse, const float* u, const float* origin,
+                       const float* dir, int64_t B, int32_t Nc, int32_t Nf, float* z,
+                       float* pts, int32_t* src, int32_t* inds, float* cdf,
+                       anr_stream_t stream);
+/* Backward into the weights through t_in_bin (bin width detached): d_z (B, Nc+Nf) and/or
+ * d_pts (B, Nc+Nf, 3) (each nullable) -> d_weights channel 0 WRITTEN (rest untouched). */
+int anr_sample_pdf_bwd(const float* weights, int64_t w_ray_stride, int32_t w_sample_stride,
+                       const float* z_coarse, const float* u, const float* dir,
+                       const int32_t* src, const int32_t* inds, const float* cdf, int64_t B,
+                       int32_t Nc, int32_t Nf, const float* d_z, const float* d_pts,
+                       float* d_weights, anr_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * K8: transmittance / alpha-composite integrator, render + render_with_surface

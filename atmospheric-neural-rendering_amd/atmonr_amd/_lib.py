@@ -108,6 +108,7 @@ _SIGNATURES = {
         [_P, _P, _P, _P, _P, c_int64, c_int32, _P, _P, POINTER(PrepParams), _P, _P],
     ),
     "anr_preprocess_points": (c_int32, [_P, c_int64, POINTER(PrepParams), _P, _P]),
+    "anr_preprocess_points_f64": (c_int32, [_P, c_int64, POINTER(PrepParams), _P, _P]),
     "anr_preprocess_points_bwd": (c_int32, [_P, c_int64, POINTER(PrepParams), _P, _P, _P]),
     "anr_posenc_width": (c_int32, [POINTER(PosencDesc)]),
     "anr_posenc_fwd": (c_int32, [POINTER(PosencDesc), _P, c_int64, c_int64, _P, c_int64, _P]),

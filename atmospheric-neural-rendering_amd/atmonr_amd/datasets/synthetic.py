@@ -15,7 +15,8 @@ the same ray pipeline as ``HARP2Dataset`` (harp2.py:26-429):
 
 The object exposes the attributes and methods the pipelines and the trainer use from
 ``HARP2Dataset``: ``config``, ``max_i``, ``lat``/``lon``/``alt``, ``scale``, ``offset``,
-``get_point_preprocessor``, ``__getbatch__``, ``__len__``, ``get_image_metrics``.
+``get_point_preprocessor``, ``__getbatch__``, ``__len__``, ``get_image_metrics``,
+``get_rgb``, ``target_image`` (the progress tracker's target cube, harp2.py:259-295).
 """
 
 from __future__ import annotations
@@ -26,6 +27,7 @@ from dataclasses import dataclass
 import torch
 
 from .. import _lib
+from ..metrics import image_metrics
 from ..geospatial.wgs_84 import filter_rays, get_rays, normalize_rays
 from ..samplers import preprocess_points
 
@@ -127,6 +129,10 @@ class SyntheticHARP2Dataset:
             vals = torch.linspace(-max_abs_view_angle, max_abs_view_angle, k) if k > 1 else torch.zeros(1)
             angles[sel] = vals.double()
         self.view_angles = angles
+        # nadir-most view of red, green and blue for RGB previews (rgb_mode "nadir",
+        # harp2.py:491-501)
+        self.best_rgb_idx = [min((i for i, bb in enumerate(irgb) if bb == b),
+                                 key=lambda i: abs(float(angles[i]))) for b in (1, 2, 3)]
         # pixel grid
         dlat = spacing_km / 111.32
         dlon = spacing_km / (111.32 * math.cos(math.radians(center[0])))
@@ -228,10 +234,24 @@ class SyntheticHARP2Dataset:
         return int(self.ray_origin_norm.shape[0])
 
     def get_image_metrics(self, pred_img: torch.Tensor, target_img: torch.Tensor) -> dict:
-        """PSNR per view exactly as harp2.py:310-335 (torchmetrics' formula inlined)."""
-        pred = torch.clip(pred_img / self.max_i, 0, 1)
-        target = target_img / self.max_i
-        data_range = (target.max() - target.min()).item()
-        mse = ((pred - target) ** 2).mean(dim=(1, 2))
-        psnr = 10.0 * torch.log10(torch.tensor(data_range, dtype=mse.dtype) ** 2 / mse)
-        return {"PSNR": psnr.cpu().tolist(), "PSNR_mean": psnr[~torch.isnan(psnr)].mean().item()}
+        """PSNR / SSIM per view as harp2.py:297-335 (atmonr_amd.metrics)."""
+        return image_metrics(pred_img, target_img, self.max_i)
+
+    def target_image(self) -> torch.Tensor:
+        """(V, H, W) observed radiance, 0 where a ray was filtered (harp2.py:266-271 plus
+        the trainer's nan -> 0, trainer.py:156-157)."""
+        return self.scatter_image(self.ray_rad)
+
+    def scatter_image(self, ray_values: torch.Tensor) -> torch.Tensor:
+        """Per-ray values (n_rays,) -> (V, H, W) cube, 0 at filtered rays."""
+        V = self.view_idx.shape[0]
+        img = torch.zeros(self.img_shp[0] * self.img_shp[1] * V, device=ray_values.device,
+                          dtype=ray_values.dtype)
+        img[self.ray_filter] = ray_values
+        return img.view(*self.img_shp, V).permute(2, 0, 1)
+
+    def get_rgb(self, cube: torch.Tensor) -> torch.Tensor:
+        """harp2.py:337-348: (V, H, W) cube -> (H, W, 3) nadir RGB in [0, 1]."""
+        assert cube.shape == (self.view_idx.shape[0], *self.img_shp)
+        img = torch.clamp(cube[self.best_rgb_idx] / self.max_i, 0, 1)
+        return img.permute(1, 2, 0).contiguous()

@@ -18,14 +18,14 @@ A = 6378137.0
 B = 6356752.314245
 E = (A * A - B * B) / (A * A)     # first eccentricity squared
 E2 = (A * A - B * B) / (B * B)    # second eccentricity squared
-DEG = math.pi / 180.0
 
 
 def horizontal_to_cartesian(lat, lon, alt):
-    """(lat, lon in degrees, ellipsoidal height m) -> WGS-84 Cartesian (x, y, z)."""
-    phi, lam = lat * DEG, lon * DEG
+    """(lat, lon in degrees, ellipsoidal height m) -> WGS-84 Cartesian (x, y, z), with
+    the reference's operation order (wgs_84.py:24-53), so f64 results match bit for bit."""
+    phi, lam = lat * math.pi / 180, lon * math.pi / 180
     sphi = torch.sin(phi)
-    n = A / torch.sqrt(1 - E * sphi * sphi)
+    n = A / torch.sqrt(1 - (E * sphi ** 2))
     r = (n + alt) * torch.cos(phi)
     return r * torch.cos(lam), r * torch.sin(lam), (n * (1 - E) + alt) * sphi
 
@@ -38,14 +38,14 @@ def cartesian_to_horizontal(x, y, z):
     sb, cb = torch.sin(beta), torch.cos(beta)
     lat = torch.atan2(z + E2 * B * sb ** 3, p - E * A * cb ** 3)
     sl = torch.sin(lat)
-    n = A / torch.sqrt(1 - E * sl * sl)
+    n = A / torch.sqrt(1 - (E * sl ** 2))
     alt = x / (torch.cos(lat) * torch.cos(lon)) - n
-    return lat / DEG, lon / DEG, alt
+    return lat * 180 / math.pi, lon * 180 / math.pi, alt
 
 
 def _rotation(theta_deg, phi_deg):
     """Rotation built from (zenith, azimuth) in degrees; same sense as the reference."""
-    t, p = -theta_deg * DEG, -phi_deg * DEG
+    t, p = -theta_deg * math.pi / 180, -phi_deg * math.pi / 180
     st, ct, sp, cp = torch.sin(t), torch.cos(t), torch.sin(p), torch.cos(p)
     zero = torch.zeros_like(t)
     row0 = torch.stack([cp, -sp * ct, sp * st], dim=-1)
@@ -81,7 +81,7 @@ def get_rays(lat, lon, alt, thetav, phiv, ray_origin_height, tol=10.0, max_iters
     d = local_to_ecef(view_directions(thetav.double(), phiv.double()).reshape(-1, 3),
                       lat.reshape(-1), lon.reshape(-1))
     d = -d.view(surf.shape)
-    lens = (ray_origin_height - alt) / torch.cos(thetav * DEG).double()
+    lens = (ray_origin_height - alt) / torch.cos(thetav * math.pi / 180).double()
 
     def height(lens):
         o = surf - lens[..., None] * d

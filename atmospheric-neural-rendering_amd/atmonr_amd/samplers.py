@@ -118,8 +118,19 @@ class _PreprocessFn(torch.autograd.Function):
 
 
 def preprocess_points(pts: torch.Tensor, prep: "_lib.PrepParams") -> torch.Tensor:
-    """Apply a preprocessor to arbitrary points (..., 3); differentiable w.r.t. pts."""
+    """Apply a preprocessor to arbitrary points (..., 3); differentiable w.r.t. f32 pts.
+
+    f64 points (the extract path, scripts/extract.py:206) are preprocessed in f64 end to
+    end and returned as f32 coordinates (what the hash encoder consumes); no gradient."""
     shp = pts.shape
+    if pts.dtype == torch.float64:
+        if pts.requires_grad:
+            raise _lib.ANRError("preprocess_points: f64 points are inference-only")
+        flat = pts.reshape(-1, 3).contiguous()
+        out = torch.empty(flat.shape, device=flat.device, dtype=torch.float32)
+        call("anr_preprocess_points_f64", ptr(flat), flat.shape[0], prep, ptr(out),
+             _lib.stream(flat.device))
+        return out.view(shp)
     flat = pts.reshape(-1, 3).float().contiguous()
     return _PreprocessFn.apply(flat, prep).view(shp)
 

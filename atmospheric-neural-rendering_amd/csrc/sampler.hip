@@ -28,6 +28,7 @@ constexpr double kPi = 3.141592653589793;  // torch.pi
 struct PrepDev {
   int mode, shift_lon, ngp_remap;
   float scale_f;  // (float)scale: torch multiplies an f32 tensor by a Python float in f32
+  double scale_d;
   double offset[3];
   double lat_min, lat_range, lon_min, lon_range, h;
   float alt_compress;
@@ -40,20 +41,30 @@ __device__ __forceinline__ double py_mod(double a, double b) {
   return r;
 }
 
-// torch.clip(v, -1, 1): NaN propagates (fminf/fmaxf would drop it).
-__device__ __forceinline__ float clip1(float v) { return v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v); }
 
-// preprocess_coords for one point p (normalized scene frame, f32) -> coords (f32).
-// kClip=false stops before clip(-1, 1) (the backward's clamp mask needs the raw value).
-template <bool kClip = true>
-__device__ __forceinline__ void preprocess_point(const PrepDev& P, float px, float py,
-                                                 float pz, float* out) {
-  float cx = px, cy = py, cz = pz;
+// preprocess_coords for one point p (normalized scene frame) -> coords (f32).
+// T = float: the training path (f32 points; the result is cast to f32 before the clip and
+// the NGP remap, harp2.py:384-385). T = double: the extract path (extract.py:206 feeds
+// f64 points, so clip and remap stay in f64 and only the final value is rounded — tcnn
+// casts the encoder input to f32). kClip=false stops before clip(-1, 1) (the backward's
+// clamp mask needs the raw value).
+template <typename T = float, bool kClip = true>
+__device__ __forceinline__ void preprocess_point(const PrepDev& P, T px, T py, T pz,
+                                                 float* out) {
+  T cx = px, cy = py, cz = pz;
   if (P.mode == 1) {
-    // coords_xyz * scale (f32) + offset (f64) -> f64, harp2.py:376
-    const double x = static_cast<double>(px * P.scale_f) + P.offset[0];
-    const double y = static_cast<double>(py * P.scale_f) + P.offset[1];
-    const double z = static_cast<double>(pz * P.scale_f) + P.offset[2];
+    // coords_xyz * scale + offset (f64), harp2.py:376; an f32 tensor times a Python float
+    // is computed in f32 first
+    double x, y, z;
+    if constexpr (sizeof(T) == 4) {
+      x = static_cast<double>(px * P.scale_f) + P.offset[0];
+      y = static_cast<double>(py * P.scale_f) + P.offset[1];
+      z = static_cast<double>(pz * P.scale_f) + P.offset[2];
+    } else {
+      x = px * P.scale_d + P.offset[0];
+      y = py * P.scale_d + P.offset[1];
+      z = pz * P.scale_d + P.offset[2];
+    }
     // cartesian_to_horizontal, wgs_84.py:83-97
     const double lon = atan2(y, x);
     const double D = sqrt(x * x + y * y);
@@ -70,26 +81,26 @@ __device__ __forceinline__ void preprocess_point(const PrepDev& P, float px, flo
     const double a = 2.0 * (lat_d - P.lat_min) / P.lat_range - 1.0;
     const double b = 2.0 * (lon_d - P.lon_min) / P.lon_range - 1.0;
     const double c = 2.0 * alt / P.h - 1.0;
-    // .to(float32) then clip(-1, 1), harp2.py:384-385
-    cx = static_cast<float>(a);
-    cy = static_cast<float>(b);
-    cz = static_cast<float>(c);
+    // .to(input dtype) then clip(-1, 1), harp2.py:384-385
+    cx = static_cast<T>(a);
+    cy = static_cast<T>(b);
+    cz = static_cast<T>(c);
     if (kClip) {
-      cx = clip1(cx);
-      cy = clip1(cy);
-      cz = clip1(cz);
+      cx = cx < T(-1) ? T(-1) : (cx > T(1) ? T(1) : cx);  // NaN propagates, as torch.clip
+      cy = cy < T(-1) ? T(-1) : (cy > T(1) ? T(1) : cy);
+      cz = cz < T(-1) ? T(-1) : (cz > T(1) ? T(1) : cz);
     }
   }
   if (P.ngp_remap) {
     // pts = (pts + 1) / 2 ; pts[..., 2] /= alt_compress_factor (instant_ngp.py:149,160)
-    cx = (cx + 1.0f) / 2.0f;
-    cy = (cy + 1.0f) / 2.0f;
-    cz = (cz + 1.0f) / 2.0f;
-    cz = cz / P.alt_compress;
+    cx = (cx + T(1)) / T(2);
+    cy = (cy + T(1)) / T(2);
+    cz = (cz + T(1)) / T(2);
+    cz = cz / static_cast<T>(P.alt_compress);
   }
-  out[0] = cx;
-  out[1] = cy;
-  out[2] = cz;
+  out[0] = static_cast<float>(cx);
+  out[1] = static_cast<float>(cy);
+  out[2] = static_cast<float>(cz);
 }
 
 // ---- backward of preprocess_point (NeRF back-propagates into the sample points through
@@ -159,7 +170,7 @@ __device__ void preprocess_jacobian(const PrepDev& P, float px, float py, float 
     float val[3];  // f32 values before clip and NGP remap: torch.clamp's gradient mask
     PrepDev Q = P;
     Q.ngp_remap = 0;
-    preprocess_point<false>(Q, px, py, pz, val);
+    preprocess_point<float, false>(Q, px, py, pz, val);
     for (int j = 0; j < 3; ++j) {
       const bool pass = val[j] >= -1.0f && val[j] <= 1.0f;
       for (int k = 0; k < 3; ++k) J[j][k] = pass ? o[j].d[k] : 0.0;
@@ -217,12 +228,13 @@ __global__ void __launch_bounds__(256) sample_uniform_bins_kernel(
   }
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256) preprocess_points_kernel(
-    const float* __restrict__ pts, int64_t P_n, PrepDev P, float* __restrict__ coords) {
+    const T* __restrict__ pts, int64_t P_n, PrepDev P, float* __restrict__ coords) {
   const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (idx >= P_n) return;
   float c[3];
-  preprocess_point(P, pts[idx * 3 + 0], pts[idx * 3 + 1], pts[idx * 3 + 2], c);
+  preprocess_point<T>(P, pts[idx * 3 + 0], pts[idx * 3 + 1], pts[idx * 3 + 2], c);
   coords[idx * 3 + 0] = c[0];
   coords[idx * 3 + 1] = c[1];
   coords[idx * 3 + 2] = c[2];
@@ -234,6 +246,7 @@ static PrepDev make_prep(const anr_prep_params* p) {
   d.shift_lon = p->shift_lon;
   d.ngp_remap = p->ngp_remap;
   d.scale_f = static_cast<float>(p->scale);
+  d.scale_d = p->scale;
   for (int k = 0; k < 3; ++k) d.offset[k] = p->offset[k];
   d.lat_min = p->lat_min;
   d.lat_range = p->lat_range;
@@ -286,9 +299,24 @@ extern "C" int anr_preprocess_points(const float* pts, int64_t P_n,
   ANR_CHECK_ARG(prep->mode == 0 || prep->mode == 1, "anr_preprocess_points: bad mode");
   if (P_n == 0) return ANR_OK;
   PrepDev P = make_prep(prep);
-  hipLaunchKernelGGL(preprocess_points_kernel, dim3(ceil_div(P_n, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(preprocess_points_kernel<float>, dim3(ceil_div(P_n, 256)), dim3(256), 0,
                      as_stream(stream), pts, P_n, P, coords);
   ANR_CHECK_LAUNCH("anr_preprocess_points");
+  return ANR_OK;
+}
+
+extern "C" int anr_preprocess_points_f64(const double* pts, int64_t P_n,
+                                         const anr_prep_params* prep, float* coords,
+                                         anr_stream_t stream) {
+  using namespace anr;
+  if (P_n == 0) return ANR_OK;
+  ANR_CHECK_ARG(pts && prep && coords, "anr_preprocess_points_f64: null argument");
+  ANR_CHECK_ARG(P_n >= 0, "anr_preprocess_points_f64: negative size");
+  ANR_CHECK_ARG(prep->mode == 0 || prep->mode == 1, "anr_preprocess_points_f64: bad mode");
+  PrepDev P = make_prep(prep);
+  hipLaunchKernelGGL(preprocess_points_kernel<double>, dim3(ceil_div(P_n, 256)), dim3(256), 0,
+                     as_stream(stream), pts, P_n, P, coords);
+  ANR_CHECK_LAUNCH("anr_preprocess_points_f64");
   return ANR_OK;
 }
 

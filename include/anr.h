@@ -81,6 +81,12 @@ int anr_sample_uniform_bins(const float* origin, const float* dir, const float* 
 int anr_preprocess_points(const float* pts, int64_t P, const anr_prep_params* prep,
                           float* coords, anr_stream_t stream);
 
+/* Same for f64 points (scripts/extract.py:203-209 passes (xyz - offset) / scale in f64;
+ * the whole preprocessor, clip and NGP remap run in f64, the result is rounded to f32
+ * once, where tcnn casts the encoder input). */
+int anr_preprocess_points_f64(const double* pts, int64_t P, const anr_prep_params* prep,
+                              float* coords, anr_stream_t stream);
+
 /* Backward of the preprocessor (the NeRF pipeline back-propagates into the sample points,
  * harp2.py:372-386): d_pts (P,3) f32 WRITTEN = J^T d_coords, J from fp64 forward-mode
  * derivatives of the same formula; clip passes the gradient where -1 <= value <= 1. */

@@ -1,0 +1,85 @@
+"""Extract path on the GPU (scripts/extract.py:180-211): the f64
+preprocessor against the oracle in f64, and the batched extract loop against the same
+kernels applied to the whole grid at once."""
+
+import numpy as np
+import pytest
+import torch
+
+import __graft_entry__ as ge
+from oracle import ref_nerf
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def scene(dev):
+    from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
+
+    return SyntheticHARP2Dataset(n_views=8, img_size=48, device=dev, seed=0)
+
+
+def _oracle_coords_f64(pts64, pp, alt_compress=8.0):
+    """harp2.py:372-386 in f64 on the CPU, then the INGP remap (instant_ngp.py:220-233)
+    in f64, rounded to f32 where tcnn casts its input."""
+    c = ref_nerf.preprocess_torch(pts64.cpu(), scale=float(pp.scale),
+                                  offset=torch.tensor(pp.offset, dtype=torch.float64),
+                                  lat_min=pp.lat_min, lat_range=pp.lat_range,
+                                  lon_min=pp.lon_min, lon_range=pp.lon_range,
+                                  h0=pp.ray_origin_height, shift_lon=pp.shift_lon)
+    c = (c + 1) / 2
+    c[..., 2] = c[..., 2] / alt_compress
+    return c.float()
+
+
+def test_preprocess_f64_matches_oracle(scene, dev):
+    from atmonr_amd.samplers import preprocess_points
+
+    pp = scene.get_point_preprocessor("horizontal")
+    gen = torch.Generator().manual_seed(4)
+    pts = (torch.rand(20000, 3, generator=gen, dtype=torch.float64) * 2 - 1) * torch.tensor(
+        [1.1, 1.1, 0.4], dtype=torch.float64)
+    out = preprocess_points(pts.to(dev), pp.params(ngp_remap=True, alt_compress=8.0))
+    ref = _oracle_coords_f64(pts, pp)
+    assert out.dtype == torch.float32 and out.shape == ref.shape
+    # f64 libm (CPU) vs device f64 math: at most one f32 ulp after the final rounding
+    err = (out.cpu() - ref).abs().max().item()
+    assert err <= 1.2e-7, err
+    with pytest.raises(Exception):
+        preprocess_points(pts.to(dev).requires_grad_(True), pp.params())
+
+
+def test_extract_volume_loop(scene, dev):
+    from atmonr_amd.extract import GridExtractDataset, extract_volume
+    from atmonr_amd.geospatial.wgs_84 import horizontal_to_cartesian
+    from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
+
+    p = InstantNGPPipeline(ge._ingp_config(64), scene, seed=5)
+    p.send_tensors_to(dev)
+    p.eval()
+    grid = GridExtractDataset(scene, alt_step=2000.0)
+    A = grid.sample_alt.shape[0]
+    assert A == 11 and len(grid) == 48 * 48 * A
+    # grid points as harp2_extract.py:170-186 (CPU f64 vs device f64 math)
+    lat = grid.lat.double().cpu()
+    lon = grid.lon.double().cpu()
+    alt = grid.sample_alt.double().cpu()[None, None].expand_as(lat)
+    xyz = torch.stack(list(horizontal_to_cartesian(lat, lon, alt)), -1).view(-1, 3)
+    assert (grid.xyz.cpu() - xyz).abs().max().item() < 1e-6
+    sigma = extract_volume(p, scene, grid, batch_size=500)
+    assert sigma.shape == (len(grid), 1) and bool((sigma >= 0).all())
+    # the same kernels over the whole grid in one call
+    pts = (grid.xyz - torch.as_tensor(scene.offset, dtype=torch.float64, device=dev)) / scene.scale
+    direct = p.extract(pts).float() / scene.scale
+    assert torch.equal(sigma, direct)
+    # the density MLP sees oracle coordinates (to 1 f32 ulp)
+    coords = _oracle_coords_f64(pts.cpu(), scene.get_point_preprocessor("horizontal"))
+    with torch.no_grad():
+        out = p.pos_mlp(p.pos_encoder(coords.to(dev)))
+    ref_sigma = torch.clip(out[:, :1].float(), min=0) / scene.scale
+    assert (sigma - ref_sigma).abs().max().item() <= 1e-3 * ref_sigma.abs().max().item() + 1e-12
+    # dump round trip
+    path = "/tmp/anr_extract_test.npz"
+    grid.dump(path, sigma)
+    d = np.load(path)
+    assert d["extinction"].shape == (48, 48, A, 1) and d["sample_alt"].shape == (A,)

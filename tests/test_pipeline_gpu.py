@@ -72,3 +72,27 @@ def test_extract(scene, dev):
     pts = torch.rand(1000, 3, device=dev) * 0.2 - 0.1
     sigma = p.extract(pts)
     assert sigma.shape == (1000, 1) and (sigma >= 0).all()
+
+
+def test_trainer_instant_ngp(scene, dev, tmp_path):
+    """trainer.py:91-187 on the GPU path: fixed-decay schedule, device progress buffers,
+    per-epoch PSNR rising, weights_only checkpoint resume."""
+    from atmonr_amd.trainer import Trainer
+
+    p = _pipe(scene, dev, fused=True, dtype=torch.float16)
+    cfg = {"batch_size": 2048, "num_iters": 40, "print_frequency": 10, "all_gpu": True,
+           "num_workers": 0,
+           "optimizer": {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2},
+           "scheduler": {"type": "fixed", "gamma": 0.33, "decay_start": 20, "decay_interval": 10}}
+    tr = Trainer(cfg, scene, p, log_dir=tmp_path / "log", verbose=False)
+    tr.train(tmp_path / "ckpt")
+    assert tr.iter_count == 40
+    assert tr.optimizer.param_groups[0]["lr"] == pytest.approx(1e-2 * 0.33 ** 2)
+    psnr = [h["PSNR_mean"] for h in tr.history]
+    assert len(psnr) == tr.num_epochs and psnr[-1] > psnr[0], psnr
+    q = _pipe(scene, dev, fused=True, dtype=torch.float16)
+    tr2 = Trainer(cfg, scene, q, log_dir=tmp_path / "log2", verbose=False)
+    tr2.load(tmp_path / "ckpt")
+    assert tr2.iter_count == 40
+    for m in ("pos_encoder", "pos_mlp", "dir_mlp", "surf_encoder", "surf_mlp"):
+        assert torch.equal(getattr(q, m).params, getattr(p, m).params), m

@@ -1,0 +1,179 @@
+"""Trainer host logic on CPU (trainer.py:16-274): schedules, loss log, device progress
+buffers, epoch metrics, weights_only checkpoints, and world-size-2 data parallelism
+reproducing the single-process run. A toy torch pipeline stands in for the GPU ones."""
+
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from tests.conftest import PKG  # noqa: F401  (puts the package on sys.path)
+
+
+class ToyScene:
+    """4 views of 16x16 pixels, every ray valid."""
+
+    def __init__(self, seed=0):
+        g = torch.Generator().manual_seed(seed)
+        self.device = torch.device("cpu")
+        self.img_shp = (16, 16)
+        self.view_idx = torch.arange(4)
+        n = 16 * 16 * 4
+        self.ray_filter = torch.ones(n, dtype=torch.bool)
+        self.origin = torch.randn(n, 3, generator=g)
+        self.ray_irgb_idx = torch.arange(n) % 4
+        self.ray_rad = (self.origin.sum(1) + 2).clamp(min=0.1)
+        self.max_i = float(self.ray_rad.max())
+
+    def __len__(self):
+        return self.ray_rad.shape[0]
+
+    def __getbatch__(self, idx):
+        return {"origin": self.origin[idx], "rad": self.ray_rad[idx], "idx": idx,
+                "irgb_idx": self.ray_irgb_idx[idx]}
+
+    def scatter_image(self, v):
+        img = torch.zeros(self.ray_filter.shape[0], dtype=v.dtype)
+        img[self.ray_filter] = v
+        return img.view(*self.img_shp, 4).permute(2, 0, 1)
+
+    def target_image(self):
+        return self.scatter_image(self.ray_rad)
+
+    def get_image_metrics(self, pred, target):
+        from atmonr_amd.metrics import image_metrics
+
+        return image_metrics(pred, target, self.max_i)
+
+
+class ToyPipeline:
+    def __init__(self, seed=0):
+        torch.manual_seed(seed)
+        self.lin = torch.nn.Linear(3, 4)
+
+    def parameters(self):
+        return self.lin.parameters()
+
+    def get_optimizer(self, cfg):
+        return torch.optim.Adam(self.parameters(), lr=cfg["lr"])
+
+    def forward(self, batch):
+        return {"color_map_fine": self.lin(batch["origin"])}
+
+    def compute_loss(self, batch, res):
+        p = torch.take_along_dim(res["color_map_fine"], batch["irgb_idx"][:, None], 1)[:, 0]
+        return F.mse_loss(p, batch["rad"])
+
+    def state_dict(self):
+        return {"lin": self.lin.state_dict()}
+
+    def load_state_dict(self, sd):
+        self.lin.load_state_dict(sd["lin"])
+
+
+def _cfg(**kw):
+    c = {"batch_size": 256, "num_iters": 20, "print_frequency": 3, "all_gpu": True,
+         "num_workers": 0, "optimizer": {"lr": 1e-2},
+         "scheduler": {"type": "fixed", "gamma": 0.5, "decay_start": 4, "decay_interval": 5}}
+    c.update(kw)
+    return c
+
+
+def test_fixed_schedule_log_and_checkpoint(tmp_path):
+    from atmonr_amd.trainer import Trainer, lr_at
+
+    scene, pipe = ToyScene(), ToyPipeline()
+    cfg = _cfg()
+    tr = Trainer(cfg, scene, pipe, log_dir=tmp_path / "log", verbose=False)
+    assert tr.num_epochs == 5  # 1024 rays / 256 = 4 steps per epoch, 20 iters
+    tr.train(tmp_path / "ckpt")
+    assert tr.iter_count == 20 and tr.epoch_idx == 5
+    assert tr.optimizer.param_groups[0]["lr"] == pytest.approx(lr_at(cfg, 4, 20))
+    assert lr_at(cfg, 4, 20) == pytest.approx(1e-2 * 0.5 ** 4)  # decays at 5, 10, 15, 20
+    log = [json.loads(line) for line in open(tmp_path / "log" / "scalars.jsonl")]
+    losses = [r for r in log if r["tag"] == "Loss"]
+    assert [r["step"] for r in losses] == list(range(20))
+    assert losses[-1]["value"] < losses[0]["value"]
+    assert sum(r["tag"] == "PSNR_mean" for r in log) == 5
+    assert len(tr.history) == 5 and tr.history[-1]["PSNR_mean"] > tr.history[0]["PSNR_mean"]
+    # every ray's prediction was recorded
+    assert bool((tr.pred_pixels["color_map_fine"] != 0).all())
+    # checkpoints hold plain types: weights_only loads, and resume restores everything
+    ck = torch.load(tmp_path / "ckpt" / "epoch_0005.pt", weights_only=True)
+    assert ck["iter_count"] == 20 and isinstance(ck["tensorboard_dir"], str)
+    tr2 = Trainer(cfg, scene, ToyPipeline(seed=1), log_dir=tmp_path / "log2", verbose=False)
+    tr2.load(tmp_path / "ckpt")
+    assert tr2.iter_count == 20 and tr2.epoch_idx == 5
+    assert torch.equal(tr2.pipeline.lin.weight, pipe.lin.weight)
+    assert tr2.optimizer.param_groups[0]["lr"] == tr.optimizer.param_groups[0]["lr"]
+
+
+def test_target_lr_schedule(tmp_path):
+    from atmonr_amd.trainer import Trainer
+
+    cfg = _cfg(num_iters=12, scheduler={"type": "target_lr", "final_lr": 1e-4})
+    tr = Trainer(cfg, ToyScene(), ToyPipeline(), log_dir=tmp_path, verbose=False)
+    tr.train()
+    assert tr.num_epochs == 3
+    assert tr.optimizer.param_groups[0]["lr"] == pytest.approx(1e-4, rel=1e-9)
+    with pytest.raises(NotImplementedError):
+        Trainer(_cfg(scheduler={"type": "cosine"}), ToyScene(), ToyPipeline(), log_dir=tmp_path)
+
+
+def test_metrics_psnr_ssim_known_values():
+    from atmonr_amd.metrics import psnr, ssim
+
+    t = torch.rand(3, 16, 16, generator=torch.Generator().manual_seed(0))
+    p = t + 0.1
+    assert torch.allclose(psnr(p, t, 1.0), torch.full((3,), 20.0, dtype=t.dtype), atol=1e-4)
+    s = ssim(t[:, None], t[:, None])
+    assert torch.allclose(s, torch.ones(3), atol=1e-6)
+    assert bool((ssim(p[:, None] * 0.5, t[:, None]) < 1).all())
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _dp_worker(rank, world, port, out):
+    import sys
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from atmonr_amd.trainer import Trainer
+
+    cfg = _cfg(num_iters=8, scheduler={"type": "target_lr", "final_lr": 1e-3})
+    tr = Trainer(cfg, ToyScene(), ToyPipeline(), log_dir=f"/tmp/anr_dp_log_{port}_{rank}",
+                 verbose=False)
+    tr.train()
+    out[rank] = ([p.detach().clone() for p in tr.pipeline.parameters()],
+                 tr.pred_pixels["color_map_fine"].clone())
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_two_rank_trainer_matches_single_process(tmp_path):
+    from atmonr_amd.trainer import Trainer
+
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_dp_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    cfg = _cfg(num_iters=8, scheduler={"type": "target_lr", "final_lr": 1e-3})
+    tr = Trainer(cfg, ToyScene(), ToyPipeline(), log_dir=tmp_path, verbose=False)
+    tr.train()
+    for r in (0, 1):
+        params, pix = out[r]
+        for a, b in zip(params, tr.pipeline.parameters()):
+            assert torch.allclose(a, b.detach(), rtol=1e-5, atol=1e-6)
+        # progress buffers combined across ranks: every ray recorded on every rank
+        assert bool((pix != 0).all())

@@ -213,10 +213,12 @@ _timer = None  # optional KernelTimer: HIP events around every entry-point call
 
 class KernelTimer:
     """Records a (start, end) torch.cuda.Event pair on the current stream around each
-    libanr_hip call, keyed by entry-point name (bench.py's per-kernel timing)."""
+    libanr_hip call, keyed by entry-point name or tag (bench.py's per-kernel timing).
+    ``only``: time just these names/tags (the other calls run without events)."""
 
-    def __init__(self):
+    def __init__(self, only: set[str] | None = None):
         self.events: dict[str, list] = {}
+        self.only = set(only) if only is not None else None
 
     def __enter__(self):
         global _timer
@@ -265,7 +267,7 @@ def call(name: str, *args, tag: str | None = None) -> int:
     """Call an entry point; raise ANRError on a non-zero status. ``tag`` names the call
     for the KernelTimer (defaults to the entry-point name)."""
     lib = load()
-    if _timer is not None:
+    if _timer is not None and (_timer.only is None or (tag or name) in _timer.only):
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record()

@@ -23,6 +23,12 @@
 #include "anr_common.h"
 
 // Profiling ablation (tools): 1 = backward without its atomics. 0 in product builds.
+#ifndef HASH_BS
+#define HASH_BS 8  // samples per prefetch batch of the v2 backward walker
+#endif
+#ifndef HASH_FBS
+#define HASH_FBS 4  // samples per coordinate prefetch batch of the forward walker
+#endif
 #ifndef HASH_EXP
 #define HASH_EXP 0
 #endif
@@ -108,6 +114,83 @@ struct LevelIdx {
   }
 };
 
+// Corner addressing for the v2 walkers, where a lane owns the x-offset b and the NC =
+// 2^(D-1) corners over dims 1..D-1. The per-dimension components of the cell are formed
+// once per cell; corner c then costs an xor (hashed) or add (dense) with compile-time
+// component choice after unrolling, and the hashed / dense choice is a select on the
+// level's flag, not a branch. The dense wrap (only for points outside [0, 1]) is one
+// rarely-taken branch for all corners.
+template <int D>
+struct LaneCorners {
+  static constexpr int NC = 1 << (D - 1);
+  __device__ static void indices(const LevelIdx<D>& li, const uint32_t* cell, int b,
+                                 uint32_t* idx) {
+    const uint32_t cx = (cell[0] + static_cast<uint32_t>(b)) * li.mul[0];
+    uint32_t c1[2], c2[2] = {0u, 0u};
+    c1[0] = cell[1] * li.mul[1];
+    c1[1] = c1[0] + li.mul[1];
+    if constexpr (D == 3) {
+      c2[0] = cell[2] * li.mul[2];
+      c2[1] = c2[0] + li.mul[2];
+    }
+    uint32_t sum[NC];
+    bool wrap = false;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      uint32_t hx = cx ^ c1[c & 1];
+      sum[c] = cx + c1[c & 1];
+      if constexpr (D == 3) {
+        hx ^= c2[c >> 1];
+        sum[c] += c2[c >> 1];
+      }
+      idx[c] = li.hashed ? (hx & (li.T - 1u)) : sum[c];
+      wrap = wrap || (!li.hashed && sum[c] >= li.T);
+    }
+    if (wrap) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (!li.hashed && sum[c] >= li.T) {
+          const uint32_t s1 = sum[c] - li.T;
+          idx[c] = s1 < li.T ? s1 : sum[c] % li.T;
+        }
+    }
+  }
+  // A corner with offset o along a dim keeps its lattice point in the new cell iff
+  // n = o + (old - new) is 0 or 1; it then becomes corner n there.
+  __device__ static bool leaves(int c, const int* dl) {
+    bool out = static_cast<unsigned>((c & 1) + dl[1]) > 1u;
+    if constexpr (D == 3) out = out || static_cast<unsigned>((c >> 1) + dl[2]) > 1u;
+    return out;
+  }
+  // Carry accumulators onto the new cell's corners, one dimension at a time with
+  // compile-time corner structure (dl = old - new per dim; all leave if x moved).
+  __device__ static void carry(const float* a, const int* dl, bool keepx, float* n) {
+    const int dy = dl[1];
+    const bool y0 = dy == 0, ym = dy == -1, yp = dy == 1;
+    float t[NC];
+#pragma unroll
+    for (int z = 0; z < NC / 2; ++z) {
+      const float a0 = a[2 * z], a1 = a[2 * z + 1];
+      t[2 * z] = y0 ? a0 : (ym ? a1 : 0.0f);
+      t[2 * z + 1] = y0 ? a1 : (yp ? a0 : 0.0f);
+    }
+    if constexpr (D == 3) {
+      const int dz = dl[2];
+      const bool z0 = dz == 0, zm = dz == -1, zp = dz == 1;
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        n[y] = z0 ? t[y] : (zm ? t[y + 2] : 0.0f);
+        n[y + 2] = z0 ? t[y + 2] : (zp ? t[y] : 0.0f);
+      }
+    } else {
+      n[0] = t[0];
+      n[1] = t[1];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) n[c] = keepx ? n[c] : 0.0f;
+  }
+};
+
 template <typename T, int F>
 struct Vec;
 template <>
@@ -190,13 +273,16 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
   for (int d = 0; d < D; ++d) cell[d] = 0u;
   float val[1 << D][F];
 
-  for (int64_t m = m0; m < m1; ++m) {
+  // All 2^D corners are gathered together on a cell change: one divergent region, so
+  // the waits for the gathers do not also wait for the younger coordinate prefetches
+  // (per-corner conditional gathers, tried, cost more than the loads they save).
+  auto step = [&](int64_t m, const float* xv) {
     float w[D];
     uint32_t g[D];
     bool same = have;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const float p = fmaf(scale, x[m * x_stride + d], 0.5f);
+      const float p = fmaf(scale, xv[d], 0.5f);
       const float fl = floorf(p);
       g[d] = static_cast<uint32_t>(static_cast<int>(fl));
       w[d] = p - fl;
@@ -225,6 +311,29 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
     }
     if constexpr ((HASH_EXP & 2) == 0) store_feat<TO, F>(out + m * out_stride + level * F, acc);
     else if (acc[0] == 12345.0f) out[0] = from_f32<TO>(acc[F - 1]);  // keep the work alive
+  };
+
+  // coordinates prefetched one batch ahead (indices clamped to the chunk: no branch)
+  constexpr int BS = HASH_FBS;
+  float xb[BS][D], xn[BS][D];
+  auto load_batch = [&](int64_t mb, float (*xo)[D]) {
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      const int64_t m = mb + j < m1 ? mb + j : m1 - 1;
+#pragma unroll
+      for (int d = 0; d < D; ++d) xo[j][d] = x[m * x_stride + d];
+    }
+  };
+  load_batch(m0, xb);
+  for (int64_t mb = m0; mb < m1; mb += BS) {
+    load_batch(mb + BS, xn);
+#pragma unroll
+    for (int j = 0; j < BS; ++j)
+      if (mb + j < m1) step(mb + j, xb[j]);
+#pragma unroll
+    for (int j = 0; j < BS; ++j)
+#pragma unroll
+      for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
   }
 }
 
@@ -484,23 +593,20 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     }
     if (!same) {
       if (have) {
-        int map[NC];
-        corner_shift<D>(cell, g, g[0] == cell[0], map);
-        float nacc[NC];
-        uint32_t comp[D][2];
-        li.dims(cell, comp);
+        uint32_t idx[NC];
+        LaneCorners<D>::indices(li, cell, b, idx);
+        const bool keepx = g[0] == cell[0];
+        int dl[D];
+        dl[0] = 0;
 #pragma unroll
-        for (int c = 0; c < NC; ++c) nacc[c] = 0.0f;
+        for (int d = 1; d < D; ++d) dl[d] = static_cast<int>(cell[d] - g[d]);
+        float nacc[NC];
+        LaneCorners<D>::carry(acc, dl, keepx, nacc);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          if (map[c] < 0) {
-            if (acc[c] != 0.0f && (HASH_EXP & 1) == 0)
-              atomicAdd(grad + static_cast<int64_t>(li.corner(comp, b | (c << 1))) * 2, acc[c]);
-          } else {
-#pragma unroll
-            for (int c2 = 0; c2 < NC; ++c2)
-              if (map[c] == c2) nacc[c2] = acc[c];
-          }
+          const bool out = !keepx || LaneCorners<D>::leaves(c, dl);
+          if (out && acc[c] != 0.0f && (HASH_EXP & 1) == 0)
+            atomicAdd(grad + static_cast<int64_t>(idx[c]) * 2, acc[c]);
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[c] = nacc[c];
@@ -521,7 +627,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
 
   // Batches of BS samples: the next batch's coordinates and gradients are loaded while
   // this one is processed (indices clamped to the chunk, so the loads need no branch).
-  constexpr int BS = 8;
+  constexpr int BS = HASH_BS;
   float xb[BS][D], xn[BS][D];
   TG gb[BS], gn[BS];
   auto load_batch = [&](int64_t mb, float (*xo)[D], TG* go) {
@@ -547,12 +653,11 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     }
   }
   if (have) {
-    uint32_t comp[D][2];
-    li.dims(cell, comp);
+    uint32_t idx[NC];
+    LaneCorners<D>::indices(li, cell, b, idx);
 #pragma unroll
     for (int c = 0; c < NC; ++c)
-      if (acc[c] != 0.0f)
-        atomicAdd(grad + static_cast<int64_t>(li.corner(comp, b | (c << 1))) * 2, acc[c]);
+      if (acc[c] != 0.0f) atomicAdd(grad + static_cast<int64_t>(idx[c]) * 2, acc[c]);
   }
 }
 

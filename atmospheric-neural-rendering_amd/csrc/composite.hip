@@ -338,15 +338,20 @@ __device__ __forceinline__ void load_block<float>(const float* p, int n, float* 
   }
 }
 
-// delta for the lane's SPL samples (graphics_utils.py:30-34); zs = z * z_scale.
+// delta for the lane's SPL samples (graphics_utils.py:30-34); zs = z * z_scale. The
+// neighbours across a lane boundary come from the adjacent lane; across a wave boundary
+// (several waves per ray) they are read from the row.
 template <int SPL>
-__device__ __forceinline__ void deltas(const float* zr, float zscale, int i0, int nvalid, int N,
-                                       int lane, float* dl) {
+__device__ __forceinline__ void deltas(const float* zrow, float zscale, int i0, int nvalid,
+                                       int N, int lane, float* dl) {
+  const float* zr = zrow + i0;
   float zs[SPL];
 #pragma unroll
   for (int j = 0; j < SPL; ++j) zs[j] = j < nvalid ? zr[j] * zscale : 0.0f;
-  const float prev = shfl_up(zs[SPL - 1], 1);  // last sample of lane-1
-  const float next = shfl_down(zs[0], 1);      // first sample of lane+1
+  float prev = shfl_up(zs[SPL - 1], 1);  // last sample of lane-1
+  float next = shfl_down(zs[0], 1);      // first sample of lane+1
+  if (lane == 0 && i0 > 0) prev = zrow[i0 - 1] * zscale;
+  if (lane == 63 && i0 + SPL < N) next = zrow[i0 + SPL] * zscale;
 #pragma unroll
   for (int j = 0; j < SPL; ++j) {
     const int i = i0 + j;
@@ -359,18 +364,46 @@ __device__ __forceinline__ void deltas(const float* zr, float zscale, int i0, in
   }
 }
 
-template <typename T, int SPL, int S>
+// Wave-level reverse affine scan returning, for lane l, the composed map of the lanes
+// > l (identity for lane 63) and the wave's total map (lane 0's inclusive composition).
+__device__ __forceinline__ void wave_affine_suffix_maps(float A, float B, int lane, float* Aex,
+                                                        float* Bex, float* Atot, float* Btot) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const float Ao = shfl_down(A, d);
+    const float Bo = shfl_down(B, d);
+    if (lane + d < 64) {
+      B = A * Bo + B;
+      A = A * Ao;
+    }
+  }
+  const float An = shfl_down(A, 1), Bn = shfl_down(B, 1);
+  *Aex = lane == 63 ? 1.0f : An;
+  *Bex = lane == 63 ? 0.0f : Bn;
+  *Atot = __shfl(A, 0);
+  *Btot = __shfl(B, 0);
+}
+
+// W waves per ray. W = 1: one wavefront per ray, 4 rays per 256-thread block, all scans
+// are shuffles. W = 4: one block per ray (SPL = N/256 per lane, a quarter of the
+// registers, four times the waves in flight); each scan is a wave scan plus the totals
+// of the other waves through LDS (one barrier per group of scans).
+template <typename T, int SPL, int S, int W>
 __global__ void __launch_bounds__(256) fwd_kernel(CompArgs a) {
   constexpr int C = 4;
+  constexpr int RPB = 4 / W;
+  __shared__ float sh_t[RPB][2][4][S];
+  __shared__ float sh_c[RPB][4][C];
   const int lane = threadIdx.x & 63;
-  const int64_t b = static_cast<int64_t>(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
-  if (b >= a.B) return;
+  const int wid = static_cast<int>(threadIdx.x >> 6);
+  const int part = wid % W, rib = wid / W;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * RPB + rib;
+  if (b >= a.B) return;  // uniform per ray (per block when W > 1)
   const int N = a.N;
-  const int i0 = lane * SPL;
+  const int i0 = (part * 64 + lane) * SPL;
   const int nvalid = max(0, min(SPL, N - i0));
-  const float* zr = a.z + b * N + i0;
   float dl[SPL], sg[SPL * S], col[SPL * C];
-  deltas<SPL>(zr, a.z_scale, i0, nvalid, N, lane, dl);
+  deltas<SPL>(a.z + b * N, a.z_scale, i0, nvalid, N, lane, dl);
   if (nvalid == SPL) {
     load_block<T>(static_cast<const T*>(a.sigma) + (b * N + i0) * S, SPL * S, sg);
     load_block<T>(static_cast<const T*>(a.color) + (b * N + i0) * C, SPL * C, col);
@@ -403,6 +436,28 @@ __global__ void __launch_bounds__(256) fwd_kernel(CompArgs a) {
     Tin[s] = wave_excl_prod(pt[s], lane);
     Stot[s] = wave_prod(pom[s]);
   }
+  if constexpr (W > 1) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const float tot = wave_prod(pt[s]);
+      if (lane == 0) {
+        sh_t[rib][0][part][s] = tot;
+        sh_t[rib][1][part][s] = Stot[s];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      float pre = 1.0f, all = 1.0f;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        if (w < part) pre *= sh_t[rib][0][w][s];
+        all *= sh_t[rib][1][w][s];
+      }
+      Tin[s] *= pre;
+      Stot[s] = all;
+    }
+  }
   float cm[C] = {0.0f, 0.0f, 0.0f, 0.0f};
   T* wout = a.weights ? static_cast<T*>(a.weights) + (b * N + i0) * S : nullptr;
   T* aout = a.alpha ? static_cast<T*>(a.alpha) + (b * N + i0) * S : nullptr;
@@ -421,31 +476,52 @@ __global__ void __launch_bounds__(256) fwd_kernel(CompArgs a) {
 #pragma unroll
     for (int c = 0; c < C; ++c) cm[c] += col[j * C + c] * w[S == 1 ? 0 : c];
   }
+  float atmo[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const float atmo = wave_sum(cm[c]);
-    float surf = 0.0f;
-    if (a.color_surf) surf = Stot[S == 1 ? 0 : c] * ldv(static_cast<const T*>(a.color_surf), b * C + c);
+  for (int c = 0; c < C; ++c) atmo[c] = wave_sum(cm[c]);
+  if constexpr (W > 1) {
     if (lane == 0) {
-      static_cast<T*>(a.color_map)[b * C + c] = from_f32<T>(atmo + surf);
-      if (a.atmo) static_cast<T*>(a.atmo)[b * C + c] = from_f32<T>(atmo);
+#pragma unroll
+      for (int c = 0; c < C; ++c) sh_c[rib][part][c] = atmo[c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float t = 0.0f;
+#pragma unroll
+      for (int w = 0; w < W; ++w) t += sh_c[rib][w][c];
+      atmo[c] = t;
+    }
+  }
+  if (part == 0 && lane == 0) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float surf = 0.0f;
+      if (a.color_surf) surf = Stot[S == 1 ? 0 : c] * ldv(static_cast<const T*>(a.color_surf), b * C + c);
+      static_cast<T*>(a.color_map)[b * C + c] = from_f32<T>(atmo[c] + surf);
+      if (a.atmo) static_cast<T*>(a.atmo)[b * C + c] = from_f32<T>(atmo[c]);
       if (a.surf) static_cast<T*>(a.surf)[b * C + c] = from_f32<T>(surf);
     }
   }
 }
 
-template <typename T, int SPL, int S>
+template <typename T, int SPL, int S, int W>
 __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
   constexpr int C = 4;
+  constexpr int RPB = 4 / W;
+  // per wave: totals of pt, pom and the wave's affine map (A, B); boundary dD values
+  __shared__ float sh_t[RPB][4][4][S];
+  __shared__ float sh_d[RPB][4][2];
   const int lane = threadIdx.x & 63;
-  const int64_t b = static_cast<int64_t>(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
-  if (b >= a.B) return;  // wave-uniform
+  const int wid = static_cast<int>(threadIdx.x >> 6);
+  const int part = wid % W, rib = wid / W;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * RPB + rib;
+  if (b >= a.B) return;  // uniform per ray (per block when W > 1)
   const int N = a.N;
-  const int i0 = lane * SPL;
+  const int i0 = (part * 64 + lane) * SPL;
   const int nvalid = max(0, min(SPL, N - i0));
-  const float* zr = a.z + b * N + i0;
   float dl[SPL], sg[SPL * S], col[SPL * C];
-  deltas<SPL>(zr, a.z_scale, i0, nvalid, N, lane, dl);
+  deltas<SPL>(a.z + b * N, a.z_scale, i0, nvalid, N, lane, dl);
   if (nvalid == SPL) {
     load_block<T>(static_cast<const T*>(a.sigma) + (b * N + i0) * S, SPL * S, sg);
     load_block<T>(static_cast<const T*>(a.color) + (b * N + i0) * C, SPL * C, col);
@@ -503,8 +579,49 @@ __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
     Pin[s] = wave_excl_prod(pom[s], lane);
     Q[s] = wave_excl_suffix_prod(pom[s], lane);
     Stot[s] = wave_prod(pom[s]);
-    V[s] = wave_affine_suffix(A[s], Bv[s], lane);
     r[s] = 0.0f;
+  }
+  float Aex[S], Bex[S], Atot[S], Btot[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    wave_affine_suffix_maps(A[s], Bv[s], lane, &Aex[s], &Bex[s], &Atot[s], &Btot[s]);
+  if constexpr (W > 1) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const float tpt = wave_prod(pt[s]);
+      if (lane == 0) {
+        sh_t[rib][0][part][s] = tpt;
+        sh_t[rib][1][part][s] = Stot[s];
+        sh_t[rib][2][part][s] = Atot[s];
+        sh_t[rib][3][part][s] = Btot[s];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      float pre_t = 1.0f, pre_p = 1.0f, suf_p = 1.0f, all = 1.0f, xin = 0.0f;
+#pragma unroll
+      for (int w = W - 1; w >= 0; --w) {
+        const float wt = sh_t[rib][0][w][s], wp = sh_t[rib][1][w][s];
+        if (w < part) {
+          pre_t *= wt;
+          pre_p *= wp;
+        }
+        if (w > part) {
+          suf_p *= wp;
+          xin = sh_t[rib][2][w][s] * xin + sh_t[rib][3][w][s];
+        }
+        all *= wp;
+      }
+      Tin[s] *= pre_t;
+      Pin[s] *= pre_p;
+      Q[s] *= suf_p;
+      Stot[s] = all;
+      V[s] = Aex[s] * xin + Bex[s];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; ++s) V[s] = Bex[s];
   }
   if (a.color_surf) {
 #pragma unroll
@@ -538,14 +655,21 @@ __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
     }
     dD[j] = j < nvalid ? dd : 0.0f;
   }
-  if (a.d_color_surf && lane == 0) {
+  if (a.d_color_surf && part == 0 && lane == 0) {
 #pragma unroll
     for (int c = 0; c < C; ++c)
       static_cast<T*>(a.d_color_surf)[b * C + c] = from_f32<T>(Stot[S == 1 ? 0 : c] * gs[c]);
   }
   if (a.d_z) {
-    const float dprev = shfl_up(dD[SPL - 1], 1);
-    const float dnext = shfl_down(dD[0], 1);
+    float dprev = shfl_up(dD[SPL - 1], 1);
+    float dnext = shfl_down(dD[0], 1);
+    if constexpr (W > 1) {
+      if (lane == 0) sh_d[rib][part][0] = dD[0];
+      if (lane == 63) sh_d[rib][part][1] = dD[SPL - 1];
+      __syncthreads();
+      if (lane == 0 && part > 0) dprev = sh_d[rib][part - 1][1];
+      if (lane == 63 && part < W - 1) dnext = sh_d[rib][part + 1][0];
+    }
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
       const int i = i0 + j;
@@ -564,27 +688,36 @@ __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
 }  // namespace rb
 
 // Launch a register-blocked kernel if (C, S, N) is covered; returns false otherwise.
+// Rays of up to 256 samples: one wavefront each; longer rays (N <= 4096): one 4-wave
+// block each.
 template <typename T>
 static bool launch_rb(bool bwd, const CompArgs& a, hipStream_t st) {
   if (a.C != 4 || !(a.S == 1 || a.S == 4)) return false;
-  const int spl = (a.N + 63) / 64;
-  const dim3 grid(static_cast<unsigned>(ceil_div(a.B, 4))), block(256);
-#define ANR_RB(SPL, S)                                                              \
-  do {                                                                              \
-    if (bwd)                                                                        \
-      hipLaunchKernelGGL((rb::bwd_kernel<T, SPL, S>), grid, block, 0, st, a);       \
-    else                                                                            \
-      hipLaunchKernelGGL((rb::fwd_kernel<T, SPL, S>), grid, block, 0, st, a);       \
+#define ANR_RB(SPL, S, W)                                                                    \
+  do {                                                                                       \
+    const dim3 grid(static_cast<unsigned>(ceil_div(a.B, 4 / (W)))), block(256);              \
+    if (bwd)                                                                                 \
+      hipLaunchKernelGGL((rb::bwd_kernel<T, SPL, S, W>), grid, block, 0, st, a);             \
+    else                                                                                     \
+      hipLaunchKernelGGL((rb::fwd_kernel<T, SPL, S, W>), grid, block, 0, st, a);             \
   } while (0)
-#define ANR_RB_S(SPL) \
-  if (a.S == 1) ANR_RB(SPL, 1); else ANR_RB(SPL, 4); return true;
-  switch (spl) {
-    case 1: ANR_RB_S(1)
-    case 2: ANR_RB_S(2)
-    case 3: ANR_RB_S(3)
-    case 4: ANR_RB_S(4)
-    case 8: ANR_RB_S(8)
-    case 16: ANR_RB_S(16)
+#define ANR_RB_S(SPL, W) \
+  if (a.S == 1) ANR_RB(SPL, 1, W); else ANR_RB(SPL, 4, W); return true;
+  if (a.N <= 256) {
+    switch ((a.N + 63) / 64) {
+      case 1: ANR_RB_S(1, 1)
+      case 2: ANR_RB_S(2, 1)
+      case 3: ANR_RB_S(3, 1)
+      case 4: ANR_RB_S(4, 1)
+      default: return false;
+    }
+  }
+  switch ((a.N + 255) / 256) {
+    case 2: ANR_RB_S(2, 4)
+    case 3: ANR_RB_S(3, 4)
+    case 4: ANR_RB_S(4, 4)
+    case 8: ANR_RB_S(8, 4)
+    case 16: ANR_RB_S(16, 4)
     default: return false;
   }
 #undef ANR_RB_S

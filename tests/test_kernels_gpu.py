@@ -303,6 +303,31 @@ def test_composite_vs_reference(dev, comp_path, tag):
     close(cm2.float(), torch.from_numpy(g[f"{tag}_plain_cm"]), rel=rel, atol=atol)
 
 
+@pytest.mark.parametrize("N,S", [(300, 1), (700, 4), (2000, 1), (1024, 4), (200, 4)])
+def test_composite_long_rays_vs_oracle(dev, N, S):
+    """Register-blocked paths at lengths with partial last lanes: one wave per ray up to 256
+    samples, one 4-wave block per ray above (cross-wave scans through LDS)."""
+    from atmonr_amd.graphics_utils import render_with_surface
+
+    gen = torch.Generator().manual_seed(N + S)
+    B = 5
+    z = torch.sort(torch.rand(B, N, generator=gen), dim=1).values * 20
+    color = torch.rand(B, N, 4, generator=gen) * 2
+    sigma = torch.rand(B, N, S, generator=gen) * (30.0 / N)
+    cs = torch.rand(B, 4, generator=gen)
+    ins = [t.clone().requires_grad_(True) for t in (z, color, sigma, cs)]
+    ref = ref_path.render_with_surface(*ins)
+    gouts = [torch.randn(r.shape, generator=gen) for r in ref]
+    sum((r * g).sum() for r, g in zip(ref, gouts)).backward()
+    dins = [t.to(dev).requires_grad_(True) for t in (z, color, sigma, cs)]
+    out = render_with_surface(*dins)
+    for o, r in zip(out, ref):
+        close(o, r.detach(), rel=1e-4, atol=1e-6)
+    sum((o * g.to(dev)).sum() for o, g in zip(out, gouts)).backward()
+    for d, r in zip(dins, ins):
+        close(d.grad, r.grad, rel=1e-4, atol=1e-5)
+
+
 def test_composite_known_answers(dev, comp_path):
     from atmonr_amd.graphics_utils import render_with_surface
 

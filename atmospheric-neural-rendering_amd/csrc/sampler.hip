@@ -65,15 +65,23 @@ __device__ __forceinline__ void preprocess_point(const PrepDev& P, T px, T py, T
       y = py * P.scale_d + P.offset[1];
       z = pz * P.scale_d + P.offset[2];
     }
-    // cartesian_to_horizontal, wgs_84.py:83-97
+    // cartesian_to_horizontal, wgs_84.py:83-97. The sines and cosines of the angles the
+    // reference builds with atan2 are formed from the atan2 arguments instead
+    // (sin(atan2(p, q)) = p / hypot, cos = q / hypot; cos(lon) = x / D): same values to
+    // an f64 ulp or two, far below the f32 rounding of the outputs, at a third of the
+    // transcendental work. Only lon and lat themselves need atan2.
     const double lon = atan2(y, x);
     const double D = sqrt(x * x + y * y);
-    const double u = atan2(z / D, 0.0 + kA / kB);
-    const double su = sin(u), cu = cos(u);
-    const double lat = atan2(z + (kE2 * kB) * (su * su * su), D - (kE * kA) * (cu * cu * cu));
-    const double sl = sin(lat);
+    const double t = z / D, k = kA / kB;
+    const double ru = sqrt(t * t + k * k);
+    const double su = t / ru, cu = k / ru;
+    const double Y = z + (kE2 * kB) * (su * su * su);
+    const double X = D - (kE * kA) * (cu * cu * cu);
+    const double lat = atan2(Y, X);
+    const double rl = sqrt(X * X + Y * Y);
+    const double sl = Y / rl, cl = X / rl;
     const double Nr = kA / sqrt(1.0 - kE * (sl * sl));
-    const double alt = x / (cos(lat) * cos(lon)) - Nr;
+    const double alt = x / (cl * (x / D)) - Nr;
     double lat_d = lat * 180.0 / kPi;
     double lon_d = lon * 180.0 / kPi;
     if (P.shift_lon) lon_d = py_mod(lon_d, 360.0) - 180.0;  // harp2.py:379-380

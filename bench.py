@@ -36,11 +36,14 @@ MFMA_F16_PEAK_TF = 2500.0  # dense fp16/bf16 MFMA (spec, no sparsity)
 
 
 def kernel_models(pipe, M: int) -> dict:
-    """Algorithmic work per launch of each hot kernel (DESIGN.md §Rooflines).
+    """Algorithmic work per launch of each hot kernel (DESIGN.md §5).
 
-    bytes = compulsory HBM traffic: every per-sample stream read or written once, every
-    table/weight read (or read-modify-written) once per launch; gathers and atomics that
-    the L2/MALL absorb are not counted. flops = dense MFMA work at the padded widths.
+    bytes = SURVEY §8(d)'s per-sample figures (the roofline definition BASELINE.md quotes):
+    hash forward 12 B coordinates + 16 levels x 8 corners x 2 features x 2 B gathered + 64 B
+    written = 588 B; hash backward 64 B dL/dy + 12 B + 2 x 512 B gradient read-modify-write
+    = 1,100 B (no cache reuse counted, so L2/MALL hits can lift it towards or past the HBM
+    peak). compulsory_bytes = every stream read or written once and every table /
+    gradient array once per launch (the floor). flops = dense MFMA work at padded widths.
     """
     grid = pipe.pos_encoder.hash_grids[0]
     n_table = grid.desc.n_params                # f16 table entries x features
@@ -54,14 +57,10 @@ def kernel_models(pipe, M: int) -> dict:
     nb = dirm.n_output
     enc_b = 2 * grid.n_out                      # f16 features
     return {
-        # coords in, features out; table read once
-        "hash_fwd": {"bytes": M * (12 + enc_b) + 2 * n_table, "flops": 0.0,
-                     # 12 + 16 levels x 8 corners x 2 x 2 B + 64 = 588 B
-                     "survey_bytes": M * (12 + grid.n_levels * 8 * 2 * 2 + enc_b)},
-        # coords + f32 dL/denc in; f32 table gradient read-modify-written once
-        "hash_bwd": {"bytes": M * (12 + 4 * grid.n_out) + 8 * n_table, "flops": 0.0,
-                     # 64 B dL/dy + 12 B + 2 x 512 B gradient RMW = 1,100 B
-                     "survey_bytes": M * (64 + 12 + 2 * grid.n_levels * 8 * 2 * 2)},
+        "hash_fwd": {"bytes": M * (12 + grid.n_levels * 8 * 2 * 2 + enc_b), "flops": 0.0,
+                     "compulsory_bytes": M * (12 + enc_b) + 2 * n_table},
+        "hash_bwd": {"bytes": M * (64 + 12 + 2 * grid.n_levels * 8 * 2 * 2), "flops": 0.0,
+                     "compulsory_bytes": M * (12 + 4 * grid.n_out) + 8 * n_table},
         # enc in, sigma + color out
         "field_fwd": {"bytes": M * (enc_b + 4 + 4 * nb), "flops": M * f_fwd},
         # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; forward recompute + dX + dW
@@ -229,14 +228,13 @@ def main():
                         "traffic": None, "avg_ms": round(st["avg_ms"], 4),
                         "launches": st["launches"], "units_per_launch": M,
                         "algorithmic_bytes": mdl["bytes"], "algorithmic_flops": mdl["flops"]}
-            if "survey_bytes" in mdl:
-                # SURVEY §8(d)'s per-sample figure (every corner gather / gradient RMW
-                # counted, no cache reuse) beside the compulsory-bytes model above
-                sb = mdl["survey_bytes"]
-                roofline["survey_model"] = {
-                    "bytes_per_unit": sb / M, "bytes": sb,
-                    "achieved": round(sb / (st["avg_ms"] * 1e-3) / 1e9, 1),
-                    "frac": round(sb / (st["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            roofline["bytes_per_unit"] = mdl["bytes"] / M
+            if "compulsory_bytes" in mdl:
+                # the floor: each stream and the table / gradient array once per launch
+                cb = mdl["compulsory_bytes"]
+                roofline["compulsory_model"] = {
+                    "bytes": cb, "achieved": round(cb / (st["avg_ms"] * 1e-3) / 1e9, 1),
+                    "frac": round(cb / (st["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc):
                 try:

@@ -423,21 +423,46 @@ __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const
   }
 }
 
+// Raw inputs of one 16-sample tile of the forward, prefetched a tile ahead for tiles with
+// all rows in range: every lane loads its row's encoding slice and its ray's direction
+// (the four lane groups read the same direction: one cache line), nothing is computed on
+// them until the next iteration, so no wait for these loads is placed in front of the
+// current tile's MFMAs.
+struct FwdRaw {
+  h8 xe;
+  float d0, d1, d2;
+};
+
+__device__ __forceinline__ void load_fwd_raw(const Args& a, int64_t row, int g, FwdRaw& r) {
+  r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+  const uint32_t ray = static_cast<uint32_t>(row) / a.n_per_ray;
+  const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
+  r.d0 = d[0];
+  r.d1 = d[1];
+  r.d2 = d[2];
+}
+
+__device__ __forceinline__ void fwd_raw_to_rows(const FwdRaw& r, Rows& in) {
+  in.xe = r.xe;
+  in.dx = r.d0 * 2.0f - 1.0f;
+  in.dy = r.d1 * 2.0f - 1.0f;
+  in.dz = r.d2 * 2.0f - 1.0f;
+  in.dc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  in.ds = 0.0f;
+}
+
 template <int W, int NHD>
 __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
-  const int lane = threadIdx.x & 63, g = lane >> 4;
-  const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  // wave index through readfirstlane: the tile loop then runs on scalar registers
+  const int waves = blockDim.x >> 6, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   FwdWeights<W, NHD> fw;
   fw.load(a.packed, lane);
   const int64_t n_tiles = (a.M + 15) / 16;
+  const int64_t n_full = a.M / 16;  // tiles with all 16 rows in range
   const int64_t tstride = static_cast<int64_t>(gridDim.x) * waves;
   int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave;
-  Rows cur;
-  load_rows(a, tile * 16 + (lane & 15), g, false, cur);
-  for (; tile < n_tiles; tile += tstride) {
-    const int64_t row = tile * 16 + (lane & 15);
-    Rows nxt;  // next tile's inputs in flight while this one computes
-    load_rows(a, (tile + tstride) * 16 + (lane & 15), g, false, nxt);
+  auto body = [&](const Rows& cur, int64_t row) {
     Tile<W, NHD> t;
     const bool valid = row < a.M;
     tile_forward<W, NHD, 1>(fw, &cur, &valid, g, &t, NoSink{});
@@ -455,7 +480,22 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
           if (c0 + i < a.n_out) a.color[row * a.color_stride + c0 + i] = fmaxf(t.col[i], 0.0f);
       }
     }
-    cur = nxt;
+  };
+  // full tiles: the next tile's inputs are in flight while this one computes (the
+  // prefetch index is clamped, so the loop body has no branch around the loads)
+  FwdRaw nraw;
+  if (tile < n_full) load_fwd_raw(a, tile * 16 + li, g, nraw);
+  for (; tile < n_full; tile += tstride) {
+    Rows cur;
+    fwd_raw_to_rows(nraw, cur);
+    const int64_t tn = tile + tstride < n_full ? tile + tstride : tile;
+    load_fwd_raw(a, tn * 16 + li, g, nraw);
+    body(cur, tile * 16 + li);
+  }
+  for (; tile < n_tiles; tile += tstride) {  // the last, partial tile
+    Rows cur;
+    load_rows(a, tile * 16 + li, g, false, cur);
+    body(cur, tile * 16 + li);
   }
 }
 

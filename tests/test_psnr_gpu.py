@@ -1,6 +1,6 @@
 """PSNR at fixed iterations, GPU path vs the oracle (SURVEY §8 d).
 
-The NeRF pipeline (configs/nerf.json shapes) trains on an 8-view 32x32 synthetic scene on
+The NeRF pipeline (configs/nerf.json shapes) trains on an 8-view 16x16 synthetic scene on
 the GPU and, side by side, the oracle's CPU restatement of the same step (oracle/ref_nerf.py
 + ref_path.py) from the same initial weights, the same batches and the same stratified /
 pdf draws; density noise is off in both (it is the only other random input). After 0 and K
@@ -13,7 +13,7 @@ bin a fine sample lands in, so a perturbation of the coarse weights by one f32 r
 (1e-7 relative) moves the coarse gradient by ~4 % (measured on the oracle alone). Hence two
 checks:
 * strict: that gradient path detached in both runs (everything else identical) — after
-  12 Adam steps PSNR within 0.1 dB and loss within 2 % (the fine samples still move with the
+  16 Adam steps PSNR within 0.1 dB and last-batch loss (128 rays) within 5 % (the fine samples still move with the
   coarse weights' last bits, so the runs drift slowly apart; 7+ dB of training progress);
 * reference semantics (path attached): the GPU run must land within the spread of oracle
   runs whose fine-sampler weights are perturbed by one f32 rounding.
@@ -34,6 +34,11 @@ pytestmark = pytest.mark.gpu
 CFG = {"type": "NeRF", "include_height": False, "point_preprocessor": "horizontal",
        "num_bands": 4, "ray_origin_height": 20000, "sampler": {"N_c": 64, "N_f": 128},
        "encoder": {"L_x": [14, 14, 10], "L_d": 4}, "mlp_hidden_dim": 256}
+
+
+# 8 views x 16 x 16 = 2,048 rays, batches of 128: KS[-1] = 16 steps is one epoch. Sized so
+# that each oracle run (CPU, f32) takes ~15 s on 8-16 host threads.
+IMG, BATCH, KS = 16, 128, [0, 16]
 
 
 def _prep_kwargs(pp):
@@ -109,7 +114,7 @@ def _setup(dev):
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
 
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    scene = SyntheticHARP2Dataset(n_views=8, img_size=32, device=dev, seed=0)
+    scene = SyntheticHARP2Dataset(n_views=8, img_size=IMG, device=dev, seed=0)
     # NeRF colours are exp(sigmoid(.)) in (1, e): targets rescaled into that range
     scene.ray_rad = scene.ray_rad * (2.5 / scene.max_i)
     scene.max_i = 2.5
@@ -158,7 +163,7 @@ def _train(dev, scene, K, gpu, detach_pdf, perturb_seed=None, lr=5e-4):
             step = lambda b, uc, uf: orc.step({k: v.cpu() for k, v in b.items()}, uc, uf)
         target = scene.target_image()
         gen = torch.Generator().manual_seed(7)
-        batches = iter(BatchLoader(scene, 512, seed=3))
+        batches = iter(BatchLoader(scene, BATCH, seed=3))
         out, it, loss = [], 0, float("nan")
         for k in K:
             while it < k:
@@ -175,29 +180,46 @@ def _train(dev, scene, K, gpu, detach_pdf, perturb_seed=None, lr=5e-4):
         nmod.sample_pdf, ref_nerf.sample_pdf = orig_dev, orig_ref
 
 
-def test_psnr_at_fixed_iterations_matches_oracle(dev):
-    scene = _setup(dev)
-    K = [0, 12]  # < one epoch of 16 batches
-    rec = {"iterations": K}
-    # strict: the chaotic t_in_bin gradient detached in both
-    g = _train(dev, scene, K, gpu=True, detach_pdf=True)
-    o = _train(dev, scene, K, gpu=False, detach_pdf=True)
-    rec["strict"] = {"gpu": g, "oracle": o}
-    for (_, lg, pg), (_, lo, po) in zip(g, o):
-        assert abs(pg - po) < 0.1, rec
-        if lg == lg:  # not NaN (iteration 0 has no loss)
-            assert abs(lg - lo) < 2e-2 * lo, rec
-    assert g[-1][2] > g[0][2] + 1.0, rec
-    # reference semantics: within the spread of oracle runs one f32 rounding apart
-    g = _train(dev, scene, K, gpu=True, detach_pdf=False)
-    runs = [_train(dev, scene, K, gpu=False, detach_pdf=False, perturb_seed=s) for s in (1, 2, 3)]
-    rec["full"] = {"gpu": g, "oracle_perturbed": runs}
+_REC = {}
+
+
+def _dump():
     out = os.environ.get("ANR_PSNR_OUT")
     if out:
         os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
         with open(out, "w") as f:
-            json.dump(rec, f, indent=1)
+            json.dump(_REC, f, indent=1)
+
+
+# CPU oracle training dominates these tests (minutes on a GPU box's host share): the
+# per-test limit is raised above the suite's --timeout.
+@pytest.mark.timeout(900)
+def test_psnr_at_fixed_iterations_strict(dev):
+    """t_in_bin gradient detached in both: the two implementations track each other."""
+    scene = _setup(dev)
+    K = KS
+    _REC["iterations"] = K
+    g = _train(dev, scene, K, gpu=True, detach_pdf=True)
+    o = _train(dev, scene, K, gpu=False, detach_pdf=True)
+    _REC["strict"] = {"gpu": g, "oracle": o}
+    _dump()
+    for (_, lg, pg), (_, lo, po) in zip(g, o):
+        assert abs(pg - po) < 0.1, _REC
+        if lg == lg:  # not NaN (iteration 0 has no loss)
+            assert abs(lg - lo) < 5e-2 * lo, _REC
+    assert g[-1][2] > g[0][2] + 1.0, _REC
+
+
+@pytest.mark.timeout(900)
+def test_psnr_at_fixed_iterations_reference_semantics(dev):
+    """Reference semantics: within the spread of oracle runs one f32 rounding apart."""
+    scene = _setup(dev)
+    K = KS
+    g = _train(dev, scene, K, gpu=True, detach_pdf=False)
+    runs = [_train(dev, scene, K, gpu=False, detach_pdf=False, perturb_seed=s) for s in (1, 2, 3)]
+    _REC["full"] = {"gpu": g, "oracle_perturbed": runs}
+    _dump()
     ps = [r[-1][2] for r in runs]
     lo, hi = min(ps), max(ps)
     margin = max(0.5, hi - lo)
-    assert lo - margin <= g[-1][2] <= hi + margin, rec
+    assert lo - margin <= g[-1][2] <= hi + margin, _REC

@@ -29,6 +29,9 @@
 #ifndef HASH_FBS
 #define HASH_FBS 4  // samples per coordinate prefetch batch of the forward walker
 #endif
+#ifndef HASH_F3BS
+#define HASH_F3BS 4  // samples per gather batch of the v3 forward walker (f16 table)
+#endif
 #ifndef HASH_EXP
 #define HASH_EXP 0
 #endif
@@ -334,6 +337,186 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
     for (int j = 0; j < BS; ++j)
 #pragma unroll
       for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Forward v3 (F = 2): v1's thread mapping (one thread per (chunk, level)), walked in
+// batches of BS samples so that a wave pays ONE gather round trip per batch instead of
+// one per sample. v1 waited for the gathers of every sample on which any of its lanes
+// changed cell — on the fine levels that is nearly every sample. Here the cells of all BS
+// samples are formed first, the corner gathers of every sample that enters a new cell
+// are issued back to back (raw features, nothing computed on them), then the next
+// batch's coordinates; the interpolation resolves each sample's corners afterwards
+// (new gather or the previous sample's corners, a select). Same corner order and fma
+// chain as v1, so results are bit-identical to it.
+template <typename TT>
+struct RawF2;
+template <>
+struct RawF2<__half> {
+  using type = uint32_t;  // the two f16 features of one corner
+  __device__ static type load(const __half* p) { return *reinterpret_cast<const uint32_t*>(p); }
+  __device__ static type blend(type n, type o, uint32_t keep) { return (o & keep) | (n & ~keep); }
+  __device__ static void unpack(type r, float* v) {
+    const float2 f = __half22float2(__builtin_bit_cast(__half2, r));
+    v[0] = f.x;
+    v[1] = f.y;
+  }
+};
+template <>
+struct RawF2<float> {
+  using type = float2;
+  __device__ static type load(const float* p) { return *reinterpret_cast<const float2*>(p); }
+  __device__ static type blend(type n, type o, uint32_t keep) {
+    return float2{__uint_as_float((__float_as_uint(o.x) & keep) | (__float_as_uint(n.x) & ~keep)),
+                  __uint_as_float((__float_as_uint(o.y) & keep) | (__float_as_uint(n.y) & ~keep))};
+  }
+  __device__ static void unpack(type r, float* v) {
+    v[0] = r.x;
+    v[1] = r.y;
+  }
+};
+
+// All 2^D corner indices of a cell (LevelIdx::corner for every c), with the dense wrap as
+// one rarely-taken branch for the whole cell.
+template <int D>
+__device__ __forceinline__ void cell_corners(const LevelIdx<D>& li, const uint32_t* cell,
+                                             uint32_t* idx) {
+  uint32_t comp[D][2];
+  li.dims(cell, comp);
+  uint32_t sum[1 << D];
+  bool wrap = false;
+#pragma unroll
+  for (int c = 0; c < (1 << D); ++c) {
+    uint32_t hx = 0u, sm = 0u;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      hx ^= comp[d][(c >> d) & 1];
+      sm += comp[d][(c >> d) & 1];
+    }
+    sum[c] = sm;
+    idx[c] = li.hashed ? (hx & (li.T - 1u)) : sm;
+    wrap = wrap || (!li.hashed && sm >= li.T);
+  }
+  if (wrap) {
+#pragma unroll
+    for (int c = 0; c < (1 << D); ++c)
+      if (!li.hashed && sum[c] >= li.T) {
+        const uint32_t s1 = sum[c] - li.T;
+        idx[c] = s1 < li.T ? s1 : sum[c] % li.T;
+      }
+  }
+}
+
+template <int D, typename TT, typename TO, int BS>
+__global__ void __launch_bounds__(256) hashgrid_fwd_v3_kernel(
+    GridLevels G, int n_levels, int lpw, int n_groups, const float* __restrict__ x,
+    int64_t x_stride, int64_t M, int64_t K, const TT* __restrict__ table,
+    TO* __restrict__ out, int64_t out_stride) {
+  constexpr int NCR = 1 << D;
+  using R = RawF2<TT>;
+  using raw_t = typename R::type;
+  const int lane = static_cast<int>(threadIdx.x & 63);
+  const int lg = static_cast<int>(blockIdx.x % n_groups);
+  const int64_t wave_in = (static_cast<int64_t>(blockIdx.x / n_groups) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t chunk = wave_in * (64 / lpw) + lane / lpw;
+  const int level = lg * lpw + lane % lpw;
+  const int64_t m0 = chunk * K;
+  if (level >= n_levels || m0 >= M) return;
+  const int64_t m1 = m0 + K < M ? m0 + K : M;
+
+  const float scale = G.scale[level];
+  const TT* __restrict__ grid = table + static_cast<int64_t>(G.offset[level]) * 2;
+  LevelIdx<D> li;
+  li.init(G.size[level], G.res[level]);
+
+  uint32_t cell[D];
+  bool have = false;
+#pragma unroll
+  for (int d = 0; d < D; ++d) cell[d] = 0u;
+  raw_t cur[NCR];
+#pragma unroll
+  for (int c = 0; c < NCR; ++c) cur[c] = raw_t{};
+
+  float xa[BS][D], xb[BS][D];
+  auto load_batch = [&](int64_t mb, float (*xo)[D]) {
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      const int64_t m = mb + j < m1 ? mb + j : m1 - 1;  // clamped: no branch
+#pragma unroll
+      for (int d = 0; d < D; ++d) xo[j][d] = x[m * x_stride + d];
+    }
+  };
+  // one batch: coordinates xc (loaded one batch earlier), next batch's into xo
+  auto batch = [&](int64_t mb, float (*xc)[D], float (*xo)[D]) {
+    uint32_t g[BS][D];
+    float w[BS][D];
+    bool chg[BS];
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      bool same = j > 0 || have;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const float p = fmaf(scale, xc[j][d], 0.5f);
+        const float fl = floorf(p);
+        g[j][d] = static_cast<uint32_t>(static_cast<int>(fl));
+        w[j][d] = p - fl;
+        same = same && (g[j][d] == (j > 0 ? g[j - 1][d] : cell[d]));
+      }
+      chg[j] = !same;
+    }
+    // gathers of every sample that enters a new cell, all in flight together
+    raw_t nv[BS][NCR];
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+#pragma unroll
+      for (int c = 0; c < NCR; ++c) nv[j][c] = raw_t{};
+      if (chg[j]) {
+        uint32_t idx[NCR];
+        cell_corners<D>(li, g[j], idx);
+#pragma unroll
+        for (int c = 0; c < NCR; ++c) nv[j][c] = R::load(grid + static_cast<int64_t>(idx[c]) * 2);
+      }
+    }
+    load_batch(mb + BS, xo);
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      // bitwise select on a mask the optimiser cannot relate to the branch above: with a
+      // plain select it merges the two into a phi at the branch join, whose register
+      // copies then wait for each sample's gathers there
+      uint32_t keep = chg[j] ? 0u : ~0u;
+      asm volatile("" : "+v"(keep));
+#pragma unroll
+      for (int c = 0; c < NCR; ++c) cur[c] = R::blend(nv[j][c], cur[c], keep);
+      float acc[2] = {0.0f, 0.0f};
+#pragma unroll
+      for (int c = 0; c < NCR; ++c) {
+        float wt = 1.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[j][d] : 1.0f - w[j][d];
+        float v[2];
+        R::unpack(cur[c], v);
+        acc[0] = fmaf(wt, v[0], acc[0]);
+        acc[1] = fmaf(wt, v[1], acc[1]);
+      }
+      // samples past the chunk were clamped to its last one: same cell, same weights, so
+      // they store that sample's value again (no branch around the store)
+      const int64_t m = mb + j < m1 ? mb + j : m1 - 1;
+      store_feat<TO, 2>(out + m * out_stride + level * 2, acc);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) cell[d] = g[BS - 1][d];
+    have = true;
+  };
+  // uniform trip count (K is the same for every chunk; a short last chunk re-walks its
+  // last sample), so the loop runs on scalar registers and the stores need no branch.
+  // Two batches per iteration with the coordinate buffers swapped: no register copies of
+  // in-flight loads at the loop edge.
+  const int64_t n_batches = (K + BS - 1) / BS;
+  load_batch(m0, xa);
+  for (int64_t it = 0; it < n_batches; it += 2) {
+    batch(m0 + it * BS, xa, xb);
+    if (it + 1 < n_batches) batch(m0 + (it + 1) * BS, xb, xa);  // uniform
   }
 }
 
@@ -693,13 +876,17 @@ static int64_t pick_chunk_v2(int64_t M) {
 }
 
 // Kernel generation per direction. Mode 0 (default): forward v1, backward v2 (measured
-// fastest on the ray-coherent bench workload); 1: both v1; 2: both v2.
-// ANR_HASHGRID_MODE or anr_hashgrid_force_v1() selects it (test hook).
+// fastest on the ray-coherent bench workload); 1: both v1; 2: both v2; 3: forward v3
+// (F = 2; v1 otherwise), backward v2. ANR_HASHGRID_MODE or anr_hashgrid_force_v1()
+// selects it (test hook). v3 batches the gathers of BS samples (one wait per batch):
+// equal to v1 at BS = 4 and slower at 8 / 16 on the bench geometry — the forward is
+// bound by the rate of cache-line fetches its gathers cause, not by their latency.
 static int g_hashgrid_mode = [] {
   const char* e = getenv("ANR_HASHGRID_MODE");
-  return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
+  return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
 }();
 static bool fwd_v2() { return g_hashgrid_mode == 2; }
+static bool fwd_v3() { return g_hashgrid_mode == 3; }
 static bool bwd_v2() { return g_hashgrid_mode != 1; }
 
 // Levels per wavefront of the forward walker (1, 2, 4, 8, 16, 32 or 64).
@@ -749,6 +936,19 @@ static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
   const int64_t chunks = ceil_div(M, K);
   const int64_t blocks_per_group = ceil_div(ceil_div(chunks, 64 / lpw), 4);
   const dim3 grid(static_cast<unsigned>(blocks_per_group * n_groups)), block(256);
+  if (F == 2 && fwd_v3()) {
+#define ANR_HG_FWD3(TT, TO, BS)                                                             \
+  hipLaunchKernelGGL((hashgrid_fwd_v3_kernel<D, TT, TO, BS>), grid, block, 0, s, G,         \
+                     d->n_levels, lpw, n_groups, x, x_stride, M, K,                          \
+                     static_cast<const TT*>(table), static_cast<TO*>(out), out_stride)
+    if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD3(__half, __half, HASH_F3BS);
+    else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD3(__half, float, HASH_F3BS);
+    else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD3(float, __half, 4);
+    else ANR_HG_FWD3(float, float, 4);
+#undef ANR_HG_FWD3
+    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v3)");
+    return ANR_OK;
+  }
 #define ANR_HG_FWD(TT, TO)                                                                  \
   hipLaunchKernelGGL((hashgrid_fwd_kernel<D, F, TT, TO>), grid, block, 0, s, G,             \
                      d->n_levels, lpw, n_groups, x, x_stride, M, K,                          \
@@ -802,7 +1002,7 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 
 extern "C" int anr_hashgrid_force_v1(int32_t mode) {
   const int prev = anr::g_hashgrid_mode;
-  anr::g_hashgrid_mode = (mode >= 0 && mode <= 2) ? mode : 0;
+  anr::g_hashgrid_mode = (mode >= 0 && mode <= 3) ? mode : 0;
   return prev;
 }
 

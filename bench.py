@@ -1,6 +1,6 @@
 """Train-step throughput of the AtmoNR Instant-NGP hot path on MI355X.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W [--workload nerf]
 
 Workload (BASELINE.json configs[2]): configs/instant_ngp.json with a 16-level T=2^19
 hash grid and 2x64 fused MLPs, B = 8192 rays x N = 1024 samples per rank per step, on a
@@ -9,7 +9,8 @@ batch gather -> fused sampler/preprocessor -> hash grid -> MLPs -> composite -> 
 backward -> [RCCL all-reduce of the flat gradient when N > 1] -> fused AdamW.
 Data parallel over rays, one process per GPU, weak scaling (8192 rays per rank).
 
-Rank 0 prints ONE JSON line. ``roofline`` is for the kernel that takes the most time per
+``--workload nerf`` measures BASELINE configs[1] instead (configs/nerf.json, batch 4096,
+f32 library GEMMs; see run_nerf). Rank 0 prints ONE JSON line. ``roofline`` is for the kernel that takes the most time per
 step, timed with HIP events on the launch stream inside the timed region; its
 algorithmic bytes / FLOPs per launch (kernel_models) are compulsory
 HBM traffic and dense MFMA work, and the bound is whichever fraction of peak is larger. ``cpu_baseline`` times the
@@ -33,6 +34,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_F16_PEAK_TF = 2500.0  # dense fp16/bf16 MFMA (spec, no sparsity)
+MFMA_F32_PEAK_TF = 157.3   # f32-input MFMA (spec)
 
 
 def kernel_models(pipe, M: int) -> dict:
@@ -88,6 +90,107 @@ def ingp_config(variant: str, n_samples: int) -> dict:
     return cfg
 
 
+NERF_CFG = {  # configs/nerf.json "pipeline" (BASELINE configs[1])
+    "type": "NeRF", "include_height": False, "point_preprocessor": "horizontal",
+    "num_bands": 4, "ray_origin_height": 20000, "sampler": {"N_c": 64, "N_f": 128},
+    "encoder": {"L_x": [14, 14, 10], "L_d": 4}, "mlp_hidden_dim": 256}
+
+
+def nerf_mlp_flops(net, n_rows: int) -> float:
+    """Dense forward FLOPs of one AtmoNeRF over n_rows samples (every nn.Linear)."""
+    f = sum(2.0 * m.in_features * m.out_features for m in net.modules()
+            if isinstance(m, torch.nn.Linear))
+    return f * n_rows
+
+
+def run_nerf(args, ds, dev, rank, world, t_scene):
+    """configs/nerf.json train step (nerf.py:179-240 + Adam, trainer.py:99-105): coarse
+    64 stratified + fine 64+128 pdf samples per ray, two 8x256 AtmoNeRF MLPs (f32 library
+    GEMMs), f32 composite, Adam. Batch 4096 rays per rank (nerf.json trainer.batch_size).
+    The MLP FLOPs (forward + 2x backward) over the measured step time give the roofline
+    line (f32 MFMA peak): the GEMMs are rocBLAS / hipBLASLt launches inside autograd, so
+    the step time is their upper bound, not a per-kernel HIP-event average."""
+    from atmonr_amd.batch_loader import BatchLoader
+    from atmonr_amd.parallel import FlatGradBucket
+    from atmonr_amd.pipelines.factory import get_pipeline
+
+    torch.manual_seed(0)
+    batch_size = args.batch if args.batch != 8192 else 4096
+    pipe = get_pipeline(dict(NERF_CFG), ds)
+    pipe.send_tensors_to(dev)
+    opt = pipe.get_optimizer({"lr": 5e-4})
+    bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev)
+    loader = BatchLoader(ds, batch_size, shuffle=True, rank=rank, world_size=world, seed=0)
+    it = iter(loader)
+
+    def step():
+        nonlocal it
+        try:
+            batch = next(it)
+        except StopIteration:
+            it = iter(loader)
+            batch = next(it)
+        res = pipe.forward(batch)
+        loss = pipe.compute_loss(batch, res)
+        bucket.zero()
+        loss.backward()
+        bucket.all_reduce()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    final_loss = float(loss.item())
+    ms = elapsed / args.steps * 1e3
+    value = batch_size * world * args.steps / elapsed
+    nc, nf = NERF_CFG["sampler"]["N_c"], NERF_CFG["sampler"]["N_f"]
+    flops = 3.0 * (nerf_mlp_flops(pipe.nerf["coarse"], batch_size * nc)
+                   + nerf_mlp_flops(pipe.nerf["fine"], batch_size * (nc + nf)))
+    tfs = flops / (ms * 1e-3) / 1e12
+    roofline = {"kernel": "nerf_mlp_gemms (library f32 GEMMs, whole-step time)",
+                "bound": "mfma", "achieved": round(tfs, 2), "peak": MFMA_F32_PEAK_TF,
+                "unit": "TFLOP/s", "frac": round(tfs / MFMA_F32_PEAK_TF, 4), "traffic": None,
+                "algorithmic_flops": flops, "units_per_launch": batch_size,
+                "flops_per_unit": flops / batch_size}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline
+
+        cpu = cpu_baseline.run(budget_s=args.cpu_budget)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "train-step rays/sec", "value": round(value, 1), "unit": "rays/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} "
+                    f"HARP2-shaped scene, {len(ds)} rays; random-init weights)",
+            "config": {"workload": "nerf BASELINE configs[1]: configs/nerf.json (freq. "
+                                   "positional enc + 8x256 MLP, 64 coarse + 192 fine "
+                                   "samples/ray), full train step (fwd+loss+bwd+Adam)",
+                       "global_batch": batch_size * world, "parallelism": f"dp{world}"},
+            "roofline": roofline, "cpu_baseline": cpu, "final_loss": round(final_loss, 6),
+            "scene_build_s": round(t_scene, 2)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,6 +200,8 @@ def main():
     ap.add_argument("--samples", type=int, default=1024)
     ap.add_argument("--views", type=int, default=90)
     ap.add_argument("--img-size", type=int, default=512)
+    ap.add_argument("--workload", choices=["ingp", "nerf"], default="ingp",
+                    help="ingp: BASELINE configs[2] (the headline line); nerf: configs[1]")
     ap.add_argument("--variant", choices=["baseline", "committed"], default="baseline")
     ap.add_argument("--dtype", choices=["f16", "f32"], default="f16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -123,6 +228,8 @@ def main():
     ds = SyntheticHARP2Dataset(n_views=args.views, img_size=args.img_size, device=dev, seed=0)
     torch.cuda.synchronize()
     t_scene = time.time() - t0
+    if args.workload == "nerf":
+        return run_nerf(args, ds, dev, rank, world, t_scene)
     cfg = ingp_config(args.variant, args.samples)
     dtype = torch.float16 if args.dtype == "f16" else torch.float32
     pipe = InstantNGPPipeline(cfg, ds, dtype=dtype, fused=True, seed=1337)

@@ -124,8 +124,8 @@ int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x, int64_t x_strid
                      int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
 
 /* Kernel generation: 0 = default (forward v1 one-lane-per-level, backward v2
- * four-lanes-per-level), 1 = v1 both, 2 = v2 both. Test hook; process-wide. Returns the
- * previous mode. */
+ * four-lanes-per-level), 1 = v1 both, 2 = v2 both, 3 = forward v3 (batched gathers, F = 2)
+ * + backward v2. Test hook; process-wide. Returns the previous mode. */
 int anr_hashgrid_force_v1(int32_t mode);
 
 /* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)

@@ -109,11 +109,17 @@ def _grid_inputs(dev, cfg, M, coherent, seed=0):
     return x.contiguous()
 
 
-@pytest.fixture(params=["v2", "v1"])
+# hash-grid kernel generations (anr_hashgrid_force_v1 modes): "default" = forward v1 with
+# backward v2, "v2" = both v2, "v1" = both v1, "v3" = forward v3 (batched gathers) with
+# backward v2
+_HASH_MODES = {"default": 0, "v2": 2, "v1": 1, "v3": 3}
+
+
+@pytest.fixture(params=["default", "v2", "v1", "v3"])
 def hash_path(request):
     from atmonr_amd import _lib
 
-    prev = _lib.load().anr_hashgrid_force_v1(1 if request.param == "v1" else 2)
+    prev = _lib.load().anr_hashgrid_force_v1(_HASH_MODES[request.param])
     yield request.param
     _lib.load().anr_hashgrid_force_v1(prev)
 

@@ -100,9 +100,19 @@ class PosencDesc(Structure):
 
 
 _P = c_void_p
+class GatherCol(Structure):
+    """anr_gather_col (include/anr.h)."""
+
+    _fields_ = [("src", _P), ("dst", _P), ("row_bytes", c_int64)]
+
+
+GATHER_MAX_COLS = 8
+
 _SIGNATURES = {
     "anr_abi_version": (c_int32, []),
     "anr_last_error": (ctypes.c_char_p, []),
+    "anr_gather_rows": (c_int32, [_P, c_int64, c_int32, POINTER(GatherCol), _P]),
+    "anr_ingp_surface_input": (c_int32, [_P, _P, _P, c_int64, _P, _P]),
     "anr_sample_uniform_bins": (
         c_int32,
         [_P, _P, _P, _P, _P, c_int64, c_int32, _P, _P, POINTER(PrepParams), _P, _P],
@@ -301,6 +311,46 @@ def ptr(t: torch.Tensor | None) -> int | None:
 
 def stream(device: torch.device | None = None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def gather_rows(idx: torch.Tensor, sources: list[torch.Tensor]) -> list[torch.Tensor]:
+    """[src[idx] for src in sources] in one anr_gather_rows launch (contiguous sources on
+    idx's device, rows of a 4-byte multiple)."""
+    idx = idx.to(torch.int64).contiguous()
+    B = idx.shape[0]
+    outs = [torch.empty((B,) + tuple(s.shape[1:]), dtype=s.dtype, device=s.device)
+            for s in sources]
+    for k in range(0, len(sources), GATHER_MAX_COLS):
+        part = list(zip(sources, outs))[k:k + GATHER_MAX_COLS]
+        cols = (GatherCol * len(part))()
+        for c, (s, o) in zip(cols, part):
+            if not s.is_contiguous():
+                raise ANRError("gather_rows: sources must be contiguous")
+            c.src, c.dst = ptr(s), ptr(o)
+            c.row_bytes = s[0].numel() * s.element_size() if s.dim() > 1 else s.element_size()
+        call("anr_gather_rows", ptr(idx), B, len(part), cols, stream(idx.device))
+    return outs
+
+
+def compute_copy(param: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """``param.detach().to(dtype)`` without a conversion pass per forward.
+
+    The f16 copy a module computes with (tcnn keeps f16 weights next to the f32 master)
+    is cached on the parameter. It is refreshed when torch has modified the parameter
+    since (its ``_version`` moved: load_state_dict, copy_, torch optimizers); FusedAdam
+    writes it in the same pass as the parameter update and marks it current.
+    """
+    if param.dtype == dtype:
+        return param.detach()
+    sh = getattr(param, "_anr_shadow", None)
+    if sh is None or sh.dtype != dtype or sh.device != param.device or sh.shape != param.shape:
+        sh = torch.empty(param.shape, dtype=dtype, device=param.device)
+        param._anr_shadow = sh
+        param._anr_shadow_ver = None
+    if param._anr_shadow_ver != param._version:
+        sh.copy_(param.detach())
+        param._anr_shadow_ver = param._version
+    return sh
 
 
 def hashgrid_desc(n_dims: int, n_levels: int, n_features: int, base_resolution: int,

@@ -177,6 +177,8 @@ class SyntheticHARP2Dataset:
         self.ray_irgb_idx = self.irgb_idx.to(dev)[None].expand(P, V).reshape(-1)[self.ray_filter]
         self.ray_irgb_idx = self.ray_irgb_idx.contiguous()
         self.ray_idx = torch.arange(self.ray_origin_norm.shape[0], device=dev, dtype=torch.int64)
+        self.ray_origin_norm = self.ray_origin_norm.contiguous()  # row gathers (__getbatch__)
+        self.ray_alt = self.ray_alt.contiguous()
         self._prep = make_preprocessor(self.lat, self.lon, self.scale, self.offset,
                                        ray_origin_height)
 
@@ -217,16 +219,20 @@ class SyntheticHARP2Dataset:
             raise NotImplementedError(point_preprocessor)
         return self._prep
 
+    _BATCH_KEYS = ("origin", "dir", "alt", "rad", "len", "irgb_idx")
+
     def __getbatch__(self, idx: torch.Tensor) -> dict[str, torch.Tensor]:
-        return {
-            "origin": self.ray_origin_norm[idx],
-            "dir": self.ray_dir[idx],
-            "alt": self.ray_alt[idx],
-            "rad": self.ray_rad[idx],
-            "len": self.ray_len_norm[idx],
-            "idx": self.ray_idx[idx],
-            "irgb_idx": self.ray_irgb_idx[idx],
-        }
+        """harp2.py:392-420. On the GPU every field is gathered in one kernel launch;
+        ``idx`` is returned as the batch's ray indices (ray_idx is arange)."""
+        srcs = (self.ray_origin_norm, self.ray_dir, self.ray_alt, self.ray_rad,
+                self.ray_len_norm, self.ray_irgb_idx)
+        if self.device.type == "cuda" and isinstance(idx, torch.Tensor) and idx.dim() == 1:
+            out = dict(zip(self._BATCH_KEYS, _lib.gather_rows(idx, list(srcs))))
+            out["idx"] = idx.to(torch.int64)
+            return out
+        out = {k: s[idx] for k, s in zip(self._BATCH_KEYS, srcs)}
+        out["idx"] = self.ray_idx[idx]
+        return out
 
     __getitem__ = __getbatch__
 

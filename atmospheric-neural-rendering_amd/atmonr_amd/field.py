@@ -52,7 +52,7 @@ class IngpFieldFn(torch.autograd.Function):
         grid = enc_mod.hash_grids[0]
         cdt = pos_mod.dtype
         prec = _lib.F16 if cdt == torch.float16 else _lib.F32
-        t_hash = p_hash.detach().to(enc_mod.dtype)
+        t_hash = _lib.compute_copy(p_hash, enc_mod.dtype)
         dirs = dirs.float().contiguous()
 
         enc = torch.empty(M, grid.n_out, device=dev, dtype=enc_mod.dtype)
@@ -78,8 +78,8 @@ class IngpFieldFn(torch.autograd.Function):
             ctx.save_for_backward(coords, dirs, enc, packed)
             return sigma, color
         ctx.fused_field = False
-        w_pos = p_pos.detach().to(cdt)
-        w_dir = p_dir.detach().to(cdt)
+        w_pos = _lib.compute_copy(p_pos, cdt)
+        w_dir = _lib.compute_copy(p_dir, cdt)
         pos_out = torch.empty(M, pos_mod.n_output_dims, device=dev, dtype=torch.float32)
         call("anr_mlp_fwd", ctypes.byref(pos_mod.desc), prec, ptr(w_pos), ptr(enc),
              dtype_code(enc.dtype), enc.stride(0), M, ptr(pos_out), _lib.F32,

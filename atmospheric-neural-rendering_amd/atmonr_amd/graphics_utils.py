@@ -35,6 +35,9 @@ class _CompositeFn(torch.autograd.Function):
              dtype_code(dt), B, N, C, S, ptr(color_map), ptr(atmo), ptr(surf), ptr(weights),
              ptr(alpha), _lib.stream(dev))
         ctx.save_for_backward(zc, color, sigma, cs)
+        # outputs the loss does not use (alpha, weights, atmo, surf in training) arrive as
+        # None instead of materialised zero tensors: the kernel skips null gradients
+        ctx.set_materialize_grads(False)
         ctx.z_scale = float(z_scale)
         ctx.has_surf = cs is not None
         ctx.z_dtype = z.dtype
@@ -57,6 +60,9 @@ class _CompositeFn(torch.autograd.Function):
 
         def prep(g):
             return None if g is None else g.to(dt).contiguous()
+
+        if g_cm is None:  # the kernel requires dL/dcolor_map
+            g_cm = torch.zeros(B, color.shape[2], device=dev, dtype=dt)
 
         need_z, need_c, need_s, need_cs = ctx.needs_input_grad[:4]
         d_color = torch.empty_like(color) if need_c else None

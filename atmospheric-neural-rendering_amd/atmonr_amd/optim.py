@@ -41,8 +41,15 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] += 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                # the f16 compute copy of the parameter (_lib.compute_copy), if a module
+                # keeps one, is written in the same pass and stays current
+                sh = getattr(p, "_anr_shadow", None)
+                if sh is not None and (sh.dtype != torch.float16 or sh.shape != p.shape):
+                    sh = None
                 call("anr_adam_step", ptr(p), ptr(g), ptr(st["exp_avg"]),
-                     ptr(st["exp_avg_sq"]), None, p.numel(), float(group["lr"]), float(b1),
-                     float(b2), float(group["eps"]), float(group["weight_decay"]),
+                     ptr(st["exp_avg_sq"]), ptr(sh), p.numel(), float(group["lr"]),
+                     float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
                      int(self.decoupled), int(st["step"].item()), 0, _lib.stream(p.device))
+                if sh is not None:
+                    p._anr_shadow_ver = p._version
         return loss

@@ -112,10 +112,12 @@ class InstantNGPPipeline(Pipeline):
         return self._forward_reference(ray_batch, u)
 
     def _surface(self, ray_batch):
-        # instant_ngp.py:143,150,173-174 (pts_surf in normalized Cartesian, then [0,1])
-        pts_surf = ray_batch["origin"] + ray_batch["dir"] * ray_batch["len"][:, None]
-        pts_surf = (pts_surf + 1) / 2
-        surf_in = torch.cat([pts_surf[:, :2], ray_batch["dir"]], dim=1)
+        # instant_ngp.py:143,150,173-174 (pts_surf in normalized Cartesian, then [0,1]);
+        # surf_in = [pts_surf[:, :2] | dir] built by one kernel, rounded as torch rounds
+        o, d, ln = (ray_batch[k].float().contiguous() for k in ("origin", "dir", "len"))
+        surf_in = torch.empty(o.shape[0], 5, device=o.device, dtype=torch.float32)
+        _lib.call("anr_ingp_surface_input", _lib.ptr(o), _lib.ptr(d), _lib.ptr(ln),
+                  o.shape[0], _lib.ptr(surf_in), _lib.stream(o.device))
         return F.relu(self.surf_mlp(self.surf_encoder(surf_in)))
 
     def _forward_fused(self, ray_batch, u=None):

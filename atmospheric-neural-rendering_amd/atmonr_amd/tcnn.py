@@ -162,7 +162,7 @@ class _EncodingFn(torch.autograd.Function):
     def forward(ctx, x, params, enc: "Encoding"):
         M = x.shape[0]
         out = torch.empty(M, enc.n_output_dims, device=x.device, dtype=enc.output_dtype)
-        p = params.detach().to(enc.dtype) if params.numel() else params
+        p = _lib.compute_copy(params, enc.dtype) if params.numel() else params
         s = _lib.stream(x.device)
         col_out = 0
         for (col_in, leaf), poff in zip(enc._leaves, enc._param_offsets):
@@ -241,7 +241,7 @@ class _NetworkFn(torch.autograd.Function):
     def forward(ctx, x, params, net: "Network"):
         M = x.shape[0]
         prec = _lib.F16 if net.dtype == torch.float16 else _lib.F32
-        p = params.detach().to(net.dtype)
+        p = _lib.compute_copy(params, net.dtype)
         out = torch.empty(M, net.n_output_dims, device=x.device, dtype=net.output_dtype)
         call("anr_mlp_fwd", ctypes.byref(net.desc), prec, ptr(p), ptr(x), dtype_code(x.dtype),
              x.stride(0), M, ptr(out), dtype_code(out.dtype), out.stride(0),

@@ -94,6 +94,27 @@ int anr_preprocess_points_bwd(const float* pts, int64_t P, const anr_prep_params
                               const float* d_coords, float* d_pts, anr_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
+ * Ray-batch glue in front of K1 (csrc/gather.hip).
+ * ------------------------------------------------------------------------------------
+ * anr_gather_rows: dst_k[r] = src_k[idx[r]] for every column k in one launch (the
+ * per-field indexing of HARP2Dataset.__getitem__ / __getbatch__, harp2.py:392-420).
+ * idx (B,) int64; a column is a row-major array of row_bytes-byte rows (multiple of 4,
+ * <= 4096); at most ANR_GATHER_MAX_COLS columns. */
+#define ANR_GATHER_MAX_COLS 8
+typedef struct {
+  const void* src;
+  void* dst;
+  int64_t row_bytes;
+} anr_gather_col;
+int anr_gather_rows(const int64_t* idx, int64_t B, int32_t n_cols, const anr_gather_col* cols,
+                    anr_stream_t stream);
+/* Instant-NGP surface-network input (instant_ngp.py:143,150,173): out (B,5) f32 =
+ * [((o + d*len) + 1) / 2 for x, y | d], with torch's f32 rounding of each op.
+ * origin, dir (B,3) f32, len (B,) f32. */
+int anr_ingp_surface_input(const float* origin, const float* dir, const float* len,
+                           int64_t B, float* out, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
  * K3 / K4: multi-resolution hash-grid encoding (tinycudann.Encoding otype "HashGrid",
  * instant_ngp.py:60-63,163; surface 2-D grid :78-80,173).
  * ------------------------------------------------------------------------------------ */

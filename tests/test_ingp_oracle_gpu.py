@@ -1,0 +1,165 @@
+"""Instant-NGP train step and PSNR at fixed iterations: GPU pipeline vs the oracle.
+
+The oracle (oracle/ref_ingp.py) restates instant_ngp.py:137-263 in float64 torch on the
+CPU with autograd, over the restated tcnn modules (ref_tcnn: tcnn semantics, unpinned
+against real tinycudann). Same initial parameters (the pipeline's state_dict), same rays
+and the same stratified draws on both sides.
+
+* step parity, f32 modules (the exact-f32 kernels): color maps within 1e-4 of the
+  largest value, loss within 1e-5 relative, z bit-exact, every module's parameter
+  gradient within 2e-3 relative L2 error (measured: 2e-6, 3e-7, 3e-6; dir MLP 7e-4);
+* step parity, f16 modules (the bench configuration: f16 tables / weights, fused field
+  kernels) against the oracle with the same f16 roundings (``half=True``): color maps
+  within 2e-2, loss within 5e-3 relative, gradients within 1e-1 relative L2 error (the
+  fused backward carries f16 gradient tiles the oracle keeps in f64; measured on MI355X:
+  color maps 3e-4, loss 2e-6, hash table 1.5e-2, dir MLP 4.4e-2, others <= 1.3e-3);
+* PSNR at fixed iterations (SURVEY §8 d): the f16 pipeline and the half-rounding oracle
+  train side by side for one epoch (8 AdamW steps, configs/instant_ngp.json optimizer)
+  on an 8-view 16x16 scene; the full-image PSNR (harp2.py:310-335) of a midpoint render
+  must agree within 0.1 dB at 0 and 8 iterations.
+With ANR_INGP_PSNR_OUT set, the measured errors and PSNRs are written there as JSON.
+"""
+
+import json
+import os
+
+import pytest
+import torch
+
+import __graft_entry__ as ge
+from oracle import ref_ingp
+
+pytestmark = pytest.mark.gpu
+
+IMG, BATCH, N, KS = 16, 256, 64, [0, 8]   # 8 views x 16 x 16 = 2,048 rays = 8 batches
+OPT = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
+TOL = {"f32": {"out": 1e-4, "loss": 1e-5, "grad": 2e-3},
+       "f16": {"out": 2e-2, "loss": 5e-3, "grad": 1e-1}}
+_REC = {}
+
+
+def _dump():
+    out = os.environ.get("ANR_INGP_PSNR_OUT")
+    if out:
+        os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+        with open(out, "w") as f:
+            json.dump(_REC, f, indent=1)
+
+
+@pytest.fixture(scope="module")
+def scene(dev):
+    from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
+
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    return SyntheticHARP2Dataset(n_views=8, img_size=IMG, device=dev, seed=0)
+
+
+def _pair(scene, dev, dtype):
+    from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
+
+    cfg = ge._ingp_config(N)
+    p = InstantNGPPipeline(cfg, scene, dtype=dtype, fused=True, seed=5)
+    p.send_tensors_to(dev)
+    pp = scene.get_point_preprocessor("horizontal")
+    o = ref_ingp.RefInstantNGP(cfg, p.state_dict(), ref_ingp.prep_kwargs(pp), p.scale,
+                               scene.max_i, half=dtype == torch.float16)
+    return p, o
+
+
+def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
+    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("prec", ["f32", "f16"])
+def test_train_step_matches_oracle(scene, dev, prec):
+    from atmonr_amd.batch_loader import BatchLoader
+
+    p, o = _pair(scene, dev, torch.float32 if prec == "f32" else torch.float16)
+    B = 200
+    batch = next(iter(BatchLoader(scene, B, seed=1)))
+    u = torch.rand(B, N, generator=torch.Generator().manual_seed(2))
+    res = p.forward(batch, u=u.to(dev))
+    loss = p.compute_loss(batch, res)
+    loss.backward()
+    cb = ref_ingp.cpu_batch(batch)
+    ro = o.forward(cb, u)
+    lo = o.loss(cb, ro)
+    lo.backward()
+    tol = TOL[prec]
+    rec = {"loss_gpu": loss.item(), "loss_oracle": lo.item()}
+    assert torch.equal(res["z_vals_fine"].cpu(), ro["z_vals_fine"])  # sampler bit-exact
+    # color maps against the largest rendered value (atmo + surf = color_map); the
+    # per-sample fields against their own largest value (recorded, not asserted)
+    cmax = ro["color_map_fine"].detach().abs().max()
+    for k in ("color_map_fine", "color_map_atmo", "color_map_surf", "color_fine",
+              "sigma_fine", "color_surf"):
+        x, y = res[k].detach().double().cpu(), ro[k].detach().double()
+        scale = cmax if k.startswith("color_map") else y.abs().max()
+        rec[k] = ((x - y).abs().max() / scale).item()
+    rec["loss_rel"] = abs(loss.item() - lo.item()) / abs(lo.item())
+    for m in ref_ingp.MODULES:
+        rec["grad_" + m] = _rel(getattr(p, m).params.grad.double().cpu(), o.params[m].grad)
+    _REC["step_" + prec] = rec
+    _dump()
+    for k in ("color_map_fine", "color_map_atmo", "color_map_surf"):
+        assert rec[k] <= tol["out"], (k, rec)
+    assert rec["loss_rel"] <= tol["loss"], rec
+    for m in ref_ingp.MODULES:
+        assert rec["grad_" + m] <= tol["grad"], (m, rec)
+
+
+def _render_psnr(fwd, scene, dev, chunk=1024):
+    """Full-image PSNR (harp2.py:310-335) of a midpoint (u = 0.5) render of every ray."""
+    n = len(scene)
+    pix = torch.empty(n)
+    with torch.no_grad():
+        for s in range(0, n, chunk):
+            idx = torch.arange(s, min(n, s + chunk), device=scene.device)
+            b = scene.__getbatch__(idx)
+            cm = fwd(b, torch.full((idx.numel(), N), 0.5))
+            pix[s:s + idx.numel()] = torch.take_along_dim(
+                cm.double().cpu(), b["irgb_idx"].cpu()[:, None], 1)[:, 0].float()
+    img = scene.scatter_image(pix.to(dev))
+    return scene.get_image_metrics(img, scene.target_image())["PSNR_mean"]
+
+
+@pytest.mark.timeout(900)
+def test_psnr_at_fixed_iterations_matches_oracle(scene, dev):
+    from atmonr_amd.batch_loader import BatchLoader
+
+    p, o = _pair(scene, dev, torch.float16)
+    opt_g, opt_o = p.get_optimizer(OPT), o.optimizer(OPT)
+
+    def fwd_g(b, u):
+        return p.forward(b, u=u.to(dev))["color_map_fine"]
+
+    def fwd_o(b, u):
+        return o.forward(ref_ingp.cpu_batch(b), u)["color_map_fine"]
+
+    gen = torch.Generator().manual_seed(7)
+    batches = iter(BatchLoader(scene, BATCH, seed=3))
+    out, it = [], 0
+    for k in KS:
+        lg = lo = float("nan")
+        while it < k:
+            b = next(batches)
+            u = torch.rand(b["origin"].shape[0], N, generator=gen)
+            lg_t = p.compute_loss(b, p.forward(b, u=u.to(dev)))
+            opt_g.zero_grad()
+            lg_t.backward()
+            opt_g.step()
+            cb = ref_ingp.cpu_batch(b)
+            lo_t = o.loss(cb, o.forward(cb, u))
+            opt_o.zero_grad()
+            lo_t.backward()
+            opt_o.step()
+            lg, lo, it = lg_t.item(), lo_t.item(), it + 1
+        out.append({"iteration": it, "loss_gpu": lg, "loss_oracle": lo,
+                    "psnr_gpu": _render_psnr(fwd_g, scene, dev),
+                    "psnr_oracle": _render_psnr(fwd_o, scene, dev)})
+    _REC["psnr"] = out
+    _dump()
+    for r in out:
+        assert abs(r["psnr_gpu"] - r["psnr_oracle"]) < 0.1, out
+    assert out[-1]["psnr_gpu"] > out[0]["psnr_gpu"] + 0.5, out

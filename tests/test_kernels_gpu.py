@@ -55,6 +55,30 @@ def test_sampler_empty_batch(dev):
     assert pts.shape == (0, 64, 3) and z.shape == (0, 64)
 
 
+@pytest.mark.parametrize("B", [0, 1, 777, 8192])
+def test_gather_rows_and_surface_input_bit_exact(dev, B):
+    """anr_gather_rows == per-field torch indexing (harp2.py:392-420); the surface input
+    kernel == the torch ops of instant_ngp.py:143,150,173, bit for bit."""
+    from atmonr_amd import _lib
+
+    g = torch.Generator().manual_seed(B)
+    R = 10000
+    srcs = [torch.randn(R, 3, generator=g), torch.randn(R, 3, generator=g),
+            torch.randn(R, generator=g).double(), torch.rand(R, generator=g),
+            torch.randint(0, 4, (R,), generator=g), torch.randn(R, 7, generator=g)]
+    srcs = [s.to(dev).contiguous() for s in srcs]
+    idx = torch.randint(0, R, (B,), generator=g).to(dev)
+    outs = _lib.gather_rows(idx, srcs)
+    for s, o in zip(srcs, outs):
+        assert o.dtype == s.dtype and torch.equal(o, s[idx])
+    o, d, ln = outs[0], outs[1], outs[3]
+    out = torch.empty(B, 5, device=dev)
+    _lib.call("anr_ingp_surface_input", _lib.ptr(o), _lib.ptr(d), _lib.ptr(ln), B,
+              _lib.ptr(out), _lib.stream(dev))
+    ps = (o + d * ln[:, None] + 1) / 2
+    assert torch.equal(out, torch.cat([ps[:, :2], d], dim=1))
+
+
 def _prep_from_golden(g, tag, remap=False, alt_compress=1.0):
     from atmonr_amd.datasets.synthetic import PointPreprocessor
 

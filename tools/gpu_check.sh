@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
-  ANR_PSNR_OUT=$OUT/psnr.json timeout -k 10 700 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || exit $?
+  ANR_PSNR_OUT=$OUT/psnr.json ANR_INGP_PSNR_OUT=$OUT/psnr_ingp.json timeout -k 10 700 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || exit $?
   timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit $?
 fi
 timeout -k 10 400 python -u bench.py ${BENCH_ARGS} > "$OUT/bench.log" 2>&1 || exit $?

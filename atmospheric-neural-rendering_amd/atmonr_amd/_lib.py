@@ -100,6 +100,8 @@ class PosencDesc(Structure):
 
 
 _P = c_void_p
+
+
 class GatherCol(Structure):
     """anr_gather_col (include/anr.h)."""
 
@@ -330,6 +332,16 @@ def gather_rows(idx: torch.Tensor, sources: list[torch.Tensor]) -> list[torch.Te
             c.row_bytes = s[0].numel() * s.element_size() if s.dim() > 1 else s.element_size()
         call("anr_gather_rows", ptr(idx), B, len(part), cols, stream(idx.device))
     return outs
+
+
+def grad_target(param: torch.nn.Parameter, dev) -> tuple[torch.Tensor, bool]:
+    """Where a backward kernel should ACCUMULATE ``param``'s gradient: its existing f32
+    ``.grad`` (direct=True: return None for it from autograd.Function.backward), else a
+    fresh zero buffer for autograd to accumulate (direct=False)."""
+    g = param.grad
+    if g is not None and g.dtype == torch.float32 and g.is_contiguous() and g.device == dev:
+        return g, True
+    return torch.zeros(param.shape, device=dev, dtype=torch.float32), False
 
 
 def compute_copy(param: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:

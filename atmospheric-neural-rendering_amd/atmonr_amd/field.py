@@ -34,11 +34,7 @@ from . import _lib
 from ._lib import call, dtype_code, ptr
 
 
-def _grad_target(param: torch.nn.Parameter, dev) -> tuple[torch.Tensor, bool]:
-    g = param.grad
-    if g is not None and g.dtype == torch.float32 and g.is_contiguous() and g.device == dev:
-        return g, True
-    return torch.zeros(param.shape, device=dev, dtype=torch.float32), False
+_grad_target = _lib.grad_target
 
 
 class IngpFieldFn(torch.autograd.Function):

@@ -16,10 +16,14 @@ from ._lib import call, ptr
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-                 decoupled: bool = True, **unused):
+                 decoupled: bool = True, zero_grad_in_step: bool = False, **unused):
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.decoupled = decoupled
+        # zero each gradient in the update pass (the next optimizer.zero_grad() is then a
+        # no-op for buffers that stay allocated, e.g. a FlatGradBucket: see mark_zero)
+        self.zero_grad_in_step = zero_grad_in_step
+        self.zeroed_buckets: list = []  # FlatGradBucket.fuse_zero_into
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -49,7 +53,11 @@ class FusedAdam(torch.optim.Optimizer):
                 call("anr_adam_step", ptr(p), ptr(g), ptr(st["exp_avg"]),
                      ptr(st["exp_avg_sq"]), ptr(sh), p.numel(), float(group["lr"]),
                      float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
-                     int(self.decoupled), int(st["step"].item()), 0, _lib.stream(p.device))
+                     int(self.decoupled), int(st["step"].item()),
+                     int(self.zero_grad_in_step), _lib.stream(p.device))
                 if sh is not None:
                     p._anr_shadow_ver = p._version
+        if self.zero_grad_in_step:
+            for b in self.zeroed_buckets:
+                b.mark_zero()
         return loss

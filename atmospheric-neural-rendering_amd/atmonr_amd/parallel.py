@@ -24,14 +24,29 @@ class FlatGradBucket:
         n = sum(p.numel() for p in self.params)
         dev = device if device is not None else self.params[0].device
         self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        self._known_zero = True
         off = 0
         for p in self.params:
             p.grad = self.flat[off:off + p.numel()].view_as(p)
             off += p.numel()
 
     def zero(self) -> None:
-        """optimizer.zero_grad(set_to_none=False) for every bucketed param in one fill."""
-        self.flat.zero_()
+        """optimizer.zero_grad(set_to_none=False) for every bucketed param in one fill
+        (skipped when the buffer is known to be zero already, see mark_zero)."""
+        if not self._known_zero:
+            self.flat.zero_()
+        self._known_zero = False  # backward is about to accumulate into it
+
+    def fuse_zero_into(self, optimizer) -> None:
+        """Let a FusedAdam over (at least) every bucketed param zero the gradients in its
+        update pass and mark this bucket zero after each step: the per-step fill goes."""
+        optimizer.zero_grad_in_step = True
+        optimizer.zeroed_buckets.append(self)
+
+    def mark_zero(self) -> None:
+        """The optimizer zeroed every gradient in its update pass (FusedAdam with
+        zero_grad_in_step over all bucketed params): the next zero() needs no fill."""
+        self._known_zero = True
 
     def all_reduce(self, group=None) -> None:
         """Average the gradient over the ranks of ``group`` (no-op when not distributed)."""

@@ -182,8 +182,10 @@ class _EncodingFn(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0]
         need_p = ctx.needs_input_grad[1]
         dx = torch.zeros(x.shape, device=x.device, dtype=torch.float32) if need_x else None
-        dparams = (torch.zeros(enc.params.shape, device=x.device, dtype=torch.float32)
-                   if need_p and enc.params.numel() else None)
+        # accumulate straight into an existing f32 .grad (e.g. a FlatGradBucket view) and
+        # return no gradient for it: autograd's own accumulation, without the extra pass
+        dparams, direct = ((_lib.grad_target(enc.params, x.device))
+                           if need_p and enc.params.numel() else (None, False))
         col_out = 0
         for (col_in, leaf), poff in zip(enc._leaves, enc._param_offsets):
             xs = x[:, col_in:col_in + leaf.n_in]
@@ -193,7 +195,7 @@ class _EncodingFn(torch.autograd.Function):
             col_out += leaf.n_out
         if dx is not None:
             dx = dx.to(x.dtype)
-        return dx, dparams, None
+        return dx, None if direct else dparams, None
 
 
 class Encoding(nn.Module):
@@ -256,7 +258,7 @@ class _NetworkFn(torch.autograd.Function):
         net: Network = ctx.net
         dout = dout.contiguous()
         prec = _lib.F16 if net.dtype == torch.float16 else _lib.F32
-        dparams = torch.zeros(net.params.shape, device=x.device, dtype=torch.float32)
+        dparams, direct = _lib.grad_target(net.params, x.device)
         din = None
         if ctx.needs_input_grad[0]:
             din = torch.empty(x.shape, device=x.device, dtype=x.dtype)
@@ -264,7 +266,7 @@ class _NetworkFn(torch.autograd.Function):
              x.stride(0), x.shape[0], ptr(dout), dtype_code(dout.dtype), dout.stride(0),
              ptr(din), dtype_code(x.dtype), x.stride(0) if din is not None else 0,
              ptr(dparams), _lib.stream(x.device))
-        return din, dparams, None
+        return din, None if direct else dparams, None
 
 
 class Network(nn.Module):

@@ -577,6 +577,19 @@ static int launch(bool bwd, const Args& a, hipStream_t st) {
   }
   const int64_t cap = bwd ? 256LL * pc : 2048;
   if (blocks > cap) blocks = cap;
+  if (bwd) {
+    // Minimum tiles per wave (profiling override ANR_MLP_BWD_MIN_TILES). On the per-ray
+    // surface network (8192 rows) 8 tiles per wave (64 waves, 64 flush adds per weight
+    // instead of 512) measured 0.104 ms against 0.057 ms with one tile per wave: the
+    // serial tile walk costs more than the contended flush saves, so the default is 1.
+    static const int64_t min_tiles = [] {
+      const char* e = getenv("ANR_MLP_BWD_MIN_TILES");
+      const long long v = e ? atoll(e) : 0;
+      return v > 0 ? static_cast<int64_t>(v) : static_cast<int64_t>(1);
+    }();
+    const int64_t by_tiles = (tiles + waves * min_tiles - 1) / (waves * min_tiles);
+    if (blocks > by_tiles) blocks = by_tiles > 0 ? by_tiles : 1;
+  }
   if (bwd)
     hipLaunchKernelGGL((bwd_kernel<TC, W, NIP, NOP, NH, MODE>), dim3(blocks), dim3(64 * waves),
                        lds, st, a);

@@ -120,6 +120,8 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
     pipe.send_tensors_to(dev)
     opt = pipe.get_optimizer({"lr": 5e-4})
     bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev)
+    if not args.no_fused_zero:
+        bucket.fuse_zero_into(opt)  # the Adam pass zeroes the bucket (no per-step fill)
     loader = BatchLoader(ds, batch_size, shuffle=True, rank=rank, world_size=world, seed=0)
     it = iter(loader)
 
@@ -207,6 +209,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--no-fused-zero", action="store_true",
+                    help="zero the gradient bucket with a fill instead of in the AdamW pass")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every kernel timed (per-kernel breakdown)")
     args = ap.parse_args()
@@ -242,6 +246,8 @@ def main():
     from atmonr_amd.parallel import FlatGradBucket
 
     bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev)
+    if not args.no_fused_zero:
+        bucket.fuse_zero_into(opt)  # the AdamW pass zeroes the bucket (no per-step fill)
 
     loader = BatchLoader(ds, args.batch, shuffle=True, rank=rank, world_size=world, seed=0)
     it = iter(loader)

@@ -96,3 +96,35 @@ def test_trainer_instant_ngp(scene, dev, tmp_path):
     assert tr2.iter_count == 40
     for m in ("pos_encoder", "pos_mlp", "dir_mlp", "surf_encoder", "surf_mlp"):
         assert torch.equal(getattr(q, m).params, getattr(p, m).params), m
+
+
+def test_bucket_zeroed_by_adam_matches_fill(scene, dev):
+    """FlatGradBucket.fuse_zero_into(FusedAdam): the AdamW pass zeroes the gradients, so
+    the per-step fill is skipped; three steps must land where the fill-per-step loop does."""
+    from atmonr_amd.batch_loader import BatchLoader
+    from atmonr_amd.parallel import FlatGradBucket
+
+    opt_cfg = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
+    runs = []
+    for fused in (False, True):
+        p = _pipe(scene, dev, fused=True, dtype=torch.float16)
+        opt = p.get_optimizer(opt_cfg)
+        bucket = FlatGradBucket([q for g in opt.param_groups for q in g["params"]], dev)
+        if fused:
+            bucket.fuse_zero_into(opt)
+        gen = torch.Generator().manual_seed(4)
+        for b in list(BatchLoader(scene, 1024, seed=2))[:3]:
+            u = torch.rand(b["origin"].shape[0], 64, generator=gen).to(dev)
+            loss = p.compute_loss(b, p.forward(b, u=u))
+            bucket.zero()
+            loss.backward()
+            opt.step()
+        if fused:
+            assert bucket.flat.abs().max().item() == 0.0
+        runs.append({m: getattr(p, m).params.detach().clone() for m in
+                     ("pos_encoder", "pos_mlp", "dir_mlp", "surf_encoder", "surf_mlp")})
+    # float atomics sum in arrival order, so a gradient that cancels to ~0 can change sign
+    # between any two runs and Adam turns that into a full lr step: compare in L2
+    for m in runs[0]:
+        a, b = runs[0][m], runs[1][m]
+        assert ((a - b).norm() / a.norm()).item() <= 1e-3, m

@@ -196,6 +196,21 @@ _SIGNATURES = {
         [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
          c_int64, _P, c_int64, _P, _P, _P],
     ),
+    "anr_ingp_field_fwd_rows": (
+        c_int32,
+        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
+         _P, c_int64, _P],
+    ),
+    "anr_ingp_field_bwd_rows": (
+        c_int32,
+        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
+         _P, c_int64, _P, c_int64, _P, _P, _P],
+    ),
+    "anr_occupancy_n_blocks": (c_int64, [c_int64]),
+    "anr_occupancy_count": (
+        c_int32, [_P, c_int64, _P, c_int32, c_int32, c_int32, c_float, _P, _P]),
+    "anr_occupancy_compact": (
+        c_int32, [_P, c_int64, _P, c_int32, c_int32, c_int32, c_float, _P, _P, _P, _P]),
     "anr_composite_force_generic": (c_int32, [c_int32]),
     "anr_composite_fwd": (
         c_int32,

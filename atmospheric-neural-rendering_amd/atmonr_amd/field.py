@@ -39,8 +39,12 @@ _grad_target = _lib.grad_target
 
 class IngpFieldFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, coords, dirs, n_per_ray: int, p_hash, p_pos, p_dir, pipe):
-        """coords (M,3) f32 in hash-grid space; dirs (B,3) f32, one per n_per_ray samples."""
+    def forward(ctx, coords, dirs, n_per_ray: int, p_hash, p_pos, p_dir, pipe, rows=None,
+                m_dense: int = 0):
+        """coords (M,3) f32 in hash-grid space; dirs (B,3) f32, one per n_per_ray samples.
+        With ``rows`` (occupancy culling, atmonr_amd.occupancy): coords are the kept
+        samples, rows (M,) int32 their indices among the m_dense ray-major samples; sigma
+        and color come back dense (m_dense rows), zero at the culled samples."""
         dev = coords.device
         s = _lib.stream(dev)
         M = coords.shape[0]
@@ -58,6 +62,9 @@ class IngpFieldFn(torch.autograd.Function):
         ctx.pipe = pipe
         ctx.n_per_ray = n_per_ray
         ctx.params = (p_hash, p_pos, p_dir)
+        ctx.rows = rows
+        if rows is not None and not (field_fused(pipe) and enc.dtype == torch.float16):
+            raise _lib.ANRError("occupancy culling needs the fused f16 field")
         if field_fused(pipe) and enc.dtype == torch.float16:
             pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
             packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc),
@@ -65,11 +72,19 @@ class IngpFieldFn(torch.autograd.Function):
             m_pos, m_dir = p_pos.detach().float(), p_dir.detach().float()  # f32 masters
             call("anr_ingp_field_pack", pdesc, ddesc, ptr(m_pos), ptr(m_dir), ptr(packed), s,
                  tag="field_pack")
-            sigma = torch.empty(M, device=dev, dtype=torch.float32)
-            color = torch.empty(M, pipe.dir_mlp.n_output_dims, device=dev, dtype=torch.float32)
-            call("anr_ingp_field_fwd", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
-                 ptr(dirs), n_per_ray, M, ptr(sigma), ptr(color), color.stride(0), s,
-                 tag="field_fwd")
+            nb = pipe.dir_mlp.n_output_dims
+            if rows is None:
+                sigma = torch.empty(M, device=dev, dtype=torch.float32)
+                color = torch.empty(M, nb, device=dev, dtype=torch.float32)
+                call("anr_ingp_field_fwd", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
+                     ptr(dirs), n_per_ray, M, ptr(sigma), ptr(color), color.stride(0), s,
+                     tag="field_fwd")
+            else:
+                sigma = torch.zeros(m_dense, device=dev, dtype=torch.float32)
+                color = torch.zeros(m_dense, nb, device=dev, dtype=torch.float32)
+                call("anr_ingp_field_fwd_rows", pdesc, ddesc, ptr(packed), ptr(enc),
+                     enc.stride(0), ptr(dirs), n_per_ray, M, ptr(rows), ptr(sigma), ptr(color),
+                     color.stride(0), s, tag="field_fwd")
             ctx.fused_field = True
             ctx.save_for_backward(coords, dirs, enc, packed)
             return sigma, color
@@ -121,7 +136,7 @@ class IngpFieldFn(torch.autograd.Function):
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
         return (None, None, None, None if direct_h else g_hash, None if direct_p else g_pos,
-                None if direct_d else g_dir, None)
+                None if direct_d else g_dir, None, None, None)
 
     @staticmethod
     def _backward_fused(ctx, d_sigma, d_color):
@@ -141,13 +156,19 @@ class IngpFieldFn(torch.autograd.Function):
         d_sigma = d_sigma.float().contiguous() if d_sigma is not None else None
         d_enc = torch.empty(M, enc.shape[1], device=dev, dtype=torch.float32)
         pdesc, ddesc = ctypes.byref(pipe.pos_mlp.desc), ctypes.byref(pipe.dir_mlp.desc)
-        call("anr_ingp_field_bwd", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
-             ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color), d_color.stride(0),
-             ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), s, tag="field_bwd")
+        if ctx.rows is None:
+            call("anr_ingp_field_bwd", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
+                 ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color), d_color.stride(0),
+                 ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), s, tag="field_bwd")
+        else:  # dL/d(sigma, color) are dense; read at the kept samples' rows
+            call("anr_ingp_field_bwd_rows", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
+                 ptr(dirs), ctx.n_per_ray, M, ptr(ctx.rows), ptr(d_sigma), ptr(d_color),
+                 d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), s,
+                 tag="field_bwd")
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
         return (None, None, None, None if direct_h else g_hash, None if direct_p else g_pos,
-                None if direct_d else g_dir, None)
+                None if direct_d else g_dir, None, None, None)
 
 
 def field_fused(pipe) -> bool:

@@ -28,6 +28,7 @@ from .. import _lib
 from ..field import IngpFieldFn
 from ..graphics_utils import render_with_surface
 from ..losses import LOSSES, indexed_loss
+from ..occupancy import OccupancyGrid, pipeline_density
 from ..optim import FusedAdam
 from ..samplers import preprocess_points, sample_and_preprocess, sample_uniform_bins
 from ..tcnn import Encoding, Network
@@ -39,7 +40,7 @@ class InstantNGPPipeline(Pipeline):
                     "surf_mlp"]
 
     def __init__(self, config: dict, dataset: Any, dtype: torch.dtype = torch.float16,
-                 fused: bool = True, seed: int = 1337) -> None:
+                 fused: bool = True, seed: int = 1337, occupancy=None) -> None:
         super().__init__(config, dataset)
         self.num_density_outputs = 1
         if self.config["multi_band_extinction"]:
@@ -75,6 +76,13 @@ class InstantNGPPipeline(Pipeline):
         if self.point_preprocessor is not None:
             self._prep_ngp = self.point_preprocessor.params(ngp_remap=True,
                                                             alt_compress=self.alt_compress)
+        # occupancy-grid culling (beyond the reference, atmonr_amd.occupancy): off unless
+        # passed in or configured; the uniform sampler stays the parity default
+        occ_cfg = self.config.get("occupancy_grid")
+        if occupancy is None and occ_cfg:
+            occupancy = OccupancyGrid.from_config(occ_cfg, self.alt_compress,
+                                                  getattr(dataset, "device", None))
+        self.occupancy = occupancy
 
     # ------------------------------------------------------------------ module plumbing
     def modules(self):
@@ -124,9 +132,19 @@ class InstantNGPPipeline(Pipeline):
         B = ray_batch["origin"].shape[0]
         N = self.config["num_samples_per_ray"]
         _, z_vals, coords = sample_and_preprocess(ray_batch, N, self._prep_ngp, u=u)
-        sigma, color = IngpFieldFn.apply(coords.view(B * N, 3), ray_batch["dir"].float(), N,
-                                         self.pos_encoder.params, self.pos_mlp.params,
-                                         self.dir_mlp.params, self)
+        occ = self.occupancy
+        if occ is not None and self.training:
+            occ.update(pipeline_density(self))
+        params = (self.pos_encoder.params, self.pos_mlp.params, self.dir_mlp.params, self)
+        if occ is not None and occ.active:
+            # only samples in occupied cells reach the hash grid and the MLPs; sigma and
+            # color come back dense (B*N rows) with zeros at the culled samples
+            rows, kept = occ.compact(coords.view(B * N, 3))
+            sigma, color = IngpFieldFn.apply(kept, ray_batch["dir"].float(), N, *params, rows,
+                                             B * N)
+        else:
+            sigma, color = IngpFieldFn.apply(coords.view(B * N, 3), ray_batch["dir"].float(), N,
+                                             *params)
         color = color.view(B, N, -1)
         sigma = sigma.view(B, N, 1)
         color_surf = self._surface(ray_batch)

@@ -211,7 +211,14 @@ struct Args {
   int64_t d_enc_stride;
   float* g_pos;
   float* g_dir;
+  // occupancy-compacted samples (nullable): row r of enc / d_enc is sample rows[r] of the
+  // dense (ray-major) arrays sigma, color, d_sigma, d_color; its ray is rows[r] / n_per_ray
+  const int32_t* rows;
 };
+
+__device__ __forceinline__ int64_t dense_row(const Args& a, int64_t row) {
+  return a.rows ? static_cast<int64_t>(a.rows[row]) : row;
+}
 
 __device__ __forceinline__ h8 cat(h4 a, h4 b) {
   return h8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -253,17 +260,18 @@ __device__ __forceinline__ void load_rows(const Args& a, int64_t row, int g, boo
   in.ds = 0.0f;
   if (row >= a.M) return;
   in.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+  const int64_t drow = dense_row(a, row);
   if (g == 0) {
-    const uint32_t ray = static_cast<uint32_t>(row) / a.n_per_ray;
+    const uint32_t ray = static_cast<uint32_t>(drow) / a.n_per_ray;
     const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
     in.dx = d[0] * 2.0f - 1.0f;
     in.dy = d[1] * 2.0f - 1.0f;
     in.dz = d[2] * 2.0f - 1.0f;
-    if (bwd && a.d_sigma) in.ds = a.d_sigma[row];
+    if (bwd && a.d_sigma) in.ds = a.d_sigma[drow];
   }
   if (bwd) {
     const int c0 = 4 * g;
-    const float* dcp = a.d_color + row * a.d_color_stride + c0;
+    const float* dcp = a.d_color + drow * a.d_color_stride + c0;
     if (c0 + 3 < a.n_out && (a.d_color_stride & 3) == 0) {
       in.dc = *reinterpret_cast<const f4*>(dcp);
     } else {
@@ -435,7 +443,7 @@ struct FwdRaw {
 
 __device__ __forceinline__ void load_fwd_raw(const Args& a, int64_t row, int g, FwdRaw& r) {
   r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
-  const uint32_t ray = static_cast<uint32_t>(row) / a.n_per_ray;
+  const uint32_t ray = static_cast<uint32_t>(dense_row(a, row)) / a.n_per_ray;
   const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
   r.d0 = d[0];
   r.d1 = d[1];
@@ -467,17 +475,18 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
     const bool valid = row < a.M;
     tile_forward<W, NHD, 1>(fw, &cur, &valid, g, &t, NoSink{});
     if (row < a.M) {
-      if (g == 0) a.sigma[row] = fmaxf(t.po[0], 0.0f);
+      const int64_t drow = dense_row(a, row);
+      if (g == 0) a.sigma[drow] = fmaxf(t.po[0], 0.0f);
       const int c0 = 4 * g;
       if (c0 + 3 < a.n_out && (a.color_stride & 3) == 0) {
         f4 v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = fmaxf(t.col[i], 0.0f);
-        *reinterpret_cast<f4*>(a.color + row * a.color_stride + c0) = v;
+        *reinterpret_cast<f4*>(a.color + drow * a.color_stride + c0) = v;
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (c0 + i < a.n_out) a.color[row * a.color_stride + c0 + i] = fmaxf(t.col[i], 0.0f);
+          if (c0 + i < a.n_out) a.color[drow * a.color_stride + c0 + i] = fmaxf(t.col[i], 0.0f);
       }
     }
   };
@@ -534,13 +543,15 @@ __global__ void __launch_bounds__(256) absmax_kernel(Args a, int64_t rows_per_wa
   const int64_t r1 = r0 + rows_per_wave < a.M ? r0 + rows_per_wave : a.M;
   float m = 0.0f;
   if (a.n_out == 4 && (a.d_color_stride & 3) == 0) {
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+    for (int64_t rr = r0 + threadIdx.x; rr < r1; rr += blockDim.x) {
+      const int64_t r = dense_row(a, rr);
       const f4 d = *reinterpret_cast<const f4*>(a.d_color + r * a.d_color_stride);
       m = fmaxf(m, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
       if (a.d_sigma) m = fmaxf(m, fabsf(a.d_sigma[r]));
     }
   } else {
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+    for (int64_t rr = r0 + threadIdx.x; rr < r1; rr += blockDim.x) {
+      const int64_t r = dense_row(a, rr);
       for (int c = 0; c < a.n_out; ++c) m = fmaxf(m, fabsf(a.d_color[r * a.d_color_stride + c]));
       if (a.d_sigma) m = fmaxf(m, fabsf(a.d_sigma[r]));
     }
@@ -569,13 +580,14 @@ struct RawRows {
 
 __device__ __forceinline__ void load_raw(const Args& a, int64_t row, int g, RawRows& r) {
   r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
-  const uint32_t ray = static_cast<uint32_t>(row) / a.n_per_ray;
+  const int64_t drow = dense_row(a, row);
+  const uint32_t ray = static_cast<uint32_t>(drow) / a.n_per_ray;
   const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
   r.d0 = d[0];
   r.d1 = d[1];
   r.d2 = d[2];
-  r.ds = a.d_sigma[row];
-  r.dc = *reinterpret_cast<const f4*>(a.d_color + row * a.d_color_stride);
+  r.ds = a.d_sigma[drow];
+  r.dc = *reinterpret_cast<const f4*>(a.d_color + drow * a.d_color_stride);
 }
 
 __device__ __forceinline__ void raw_to_rows(const RawRows& r, int g, Rows& in) {
@@ -1054,10 +1066,10 @@ extern "C" int anr_ingp_field_pack(const anr_mlp_desc* pos, const anr_mlp_desc* 
   return ANR_OK;
 }
 
-extern "C" int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                  const void* packed, const void* enc, int64_t enc_stride,
-                                  const float* dirs, int64_t n_per_ray, int64_t M, float* sigma,
-                                  float* color, int64_t color_stride, anr_stream_t stream) {
+static int field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const void* packed,
+                     const void* enc, int64_t enc_stride, const float* dirs, int64_t n_per_ray,
+                     int64_t M, const int32_t* rows, float* sigma, float* color,
+                     int64_t color_stride, anr_stream_t stream) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_fwd: unsupported pos/dir MLP pair");
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_fwd: bad M");
@@ -1080,18 +1092,18 @@ extern "C" int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* d
   a.sigma = sigma;
   a.color = color;
   a.color_stride = color_stride;
+  a.rows = rows;
   ANR_CHECK_ARG(dispatch(v, 1, a, reinterpret_cast<hipStream_t>(stream)) == 0,
                 "anr_ingp_field_fwd: no kernel for this shape");
   ANR_CHECK_LAUNCH("anr_ingp_field_fwd");
   return ANR_OK;
 }
 
-extern "C" int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                  const void* packed, const void* enc, int64_t enc_stride,
-                                  const float* dirs, int64_t n_per_ray, int64_t M,
-                                  const float* d_sigma, const float* d_color,
-                                  int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
-                                  float* g_pos, float* g_dir, anr_stream_t stream) {
+static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const void* packed,
+                     const void* enc, int64_t enc_stride, const float* dirs, int64_t n_per_ray,
+                     int64_t M, const int32_t* rows, const float* d_sigma,
+                     const float* d_color, int64_t d_color_stride, float* d_enc,
+                     int64_t d_enc_stride, float* g_pos, float* g_dir, anr_stream_t stream) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_bwd: unsupported pos/dir MLP pair");
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_bwd: bad M");
@@ -1121,11 +1133,52 @@ extern "C" int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* d
   a.d_enc_stride = d_enc_stride;
   a.g_pos = g_pos;
   a.g_dir = g_dir;
+  a.rows = rows;
   const int rc = dispatch(v, 2, a, reinterpret_cast<hipStream_t>(stream));
   ANR_CHECK_ARG(rc != 2, "anr_ingp_field_bwd: scratch allocation failed");
   ANR_CHECK_ARG(rc == 0, "anr_ingp_field_bwd: no kernel for this shape");
   ANR_CHECK_LAUNCH("anr_ingp_field_bwd");
   return ANR_OK;
+}
+
+extern "C" int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                  const void* packed, const void* enc, int64_t enc_stride,
+                                  const float* dirs, int64_t n_per_ray, int64_t M, float* sigma,
+                                  float* color, int64_t color_stride, anr_stream_t stream) {
+  return field_fwd(pos, dir, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr, sigma, color,
+                   color_stride, stream);
+}
+
+extern "C" int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                  const void* packed, const void* enc, int64_t enc_stride,
+                                  const float* dirs, int64_t n_per_ray, int64_t M,
+                                  const float* d_sigma, const float* d_color,
+                                  int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
+                                  float* g_pos, float* g_dir, anr_stream_t stream) {
+  return field_bwd(pos, dir, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr, d_sigma,
+                   d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, stream);
+}
+
+extern "C" int anr_ingp_field_fwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                       const void* packed, const void* enc, int64_t enc_stride,
+                                       const float* dirs, int64_t n_per_ray, int64_t M,
+                                       const int32_t* rows, float* sigma, float* color,
+                                       int64_t color_stride, anr_stream_t stream) {
+  ANR_CHECK_ARG(rows || M == 0, "anr_ingp_field_fwd_rows: null rows");
+  return field_fwd(pos, dir, packed, enc, enc_stride, dirs, n_per_ray, M, rows, sigma, color,
+                   color_stride, stream);
+}
+
+extern "C" int anr_ingp_field_bwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                       const void* packed, const void* enc, int64_t enc_stride,
+                                       const float* dirs, int64_t n_per_ray, int64_t M,
+                                       const int32_t* rows, const float* d_sigma,
+                                       const float* d_color, int64_t d_color_stride,
+                                       float* d_enc, int64_t d_enc_stride, float* g_pos,
+                                       float* g_dir, anr_stream_t stream) {
+  ANR_CHECK_ARG(rows || M == 0, "anr_ingp_field_bwd_rows: null rows");
+  return field_bwd(pos, dir, packed, enc, enc_stride, dirs, n_per_ray, M, rows, d_sigma,
+                   d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, stream);
 }
 
 #ifdef FIELD_STAMP

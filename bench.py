@@ -209,6 +209,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--occupancy", action="store_true",
+                    help="BASELINE configs[4]: occupancy-grid culling (beyond the reference); "
+                         "use a long --warmup so the grid has learned the scene")
+    ap.add_argument("--occ-warmup", type=int, default=100,
+                    help="steps before the occupancy grid starts culling")
     ap.add_argument("--no-fused-zero", action="store_true",
                     help="zero the gradient bucket with a fill instead of in the AdamW pass")
     ap.add_argument("--profile-steps", type=int, default=3,
@@ -236,7 +241,13 @@ def main():
         return run_nerf(args, ds, dev, rank, world, t_scene)
     cfg = ingp_config(args.variant, args.samples)
     dtype = torch.float16 if args.dtype == "f16" else torch.float32
-    pipe = InstantNGPPipeline(cfg, ds, dtype=dtype, fused=True, seed=1337)
+    occ = None
+    if args.occupancy:
+        from atmonr_amd.occupancy import OccupancyGrid
+
+        occ = OccupancyGrid((128, 128, 32), alt_compress=float(cfg["alt_compress_factor"]),
+                            warmup=args.occ_warmup, update_every=16, device=dev)
+    pipe = InstantNGPPipeline(cfg, ds, dtype=dtype, fused=True, seed=1337, occupancy=occ)
     pipe.send_tensors_to(dev)
     opt_cfg = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
     opt = pipe.get_optimizer(opt_cfg)
@@ -386,7 +397,9 @@ def main():
                 "workload": (f"instant_ngp {'BASELINE configs[2]' if args.variant == 'baseline' else 'committed configs/instant_ngp.json'}"
                              f": 16-level T=2^{T.bit_length() - 1} hash grid, 2x{width} fused "
                              f"MLP, {args.samples} samples/ray, full train step "
-                             f"(fwd+loss+bwd+AdamW)"),
+                             f"(fwd+loss+bwd+AdamW)"
+                             + (" + occupancy-grid culling (BASELINE configs[4], beyond the "
+                                "reference)" if occ is not None else "")),
                 "global_batch": args.batch * world,
                 "samples_per_ray": args.samples,
                 "parallelism": f"dp{world}",
@@ -395,6 +408,11 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kernels,
             "kernels_source": f"untimed profiling pass of {args.profile_steps} steps",
+            "occupancy": None if occ is None else {
+                "grid": list(occ.res), "threshold": occ.threshold, "warmup": occ.warmup,
+                "update_every": occ.update_every, "active": occ.active,
+                "kept_fraction_last_step": round(occ.last_fraction, 4),
+                "occupied_cells": round(occ.occupancy_fraction(), 4)},
             "final_loss": round(final_loss, 6),
             "scene_build_s": round(t_scene, 2),
         }

@@ -259,6 +259,39 @@ int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const v
                        const float* d_color, int64_t d_color_stride, float* d_enc,
                        int64_t d_enc_stride, float* g_pos, float* g_dir, anr_stream_t stream);
 
+/* The same kernels over occupancy-compacted samples (anr_occupancy_compact): row r of
+ * enc / d_enc is dense sample rows[r] (int32, ray-major index < n_rays * n_per_ray) of
+ * sigma, color, d_sigma, d_color, whose ray is rows[r] / n_per_ray. The forward writes
+ * only the listed dense rows (the caller zero-fills the rest: culled samples have
+ * sigma = 0), the backward reads dL/d(sigma, color) at those rows. */
+int anr_ingp_field_fwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                            const void* packed, const void* enc, int64_t enc_stride,
+                            const float* dirs, int64_t n_per_ray, int64_t M,
+                            const int32_t* rows, float* sigma, float* color,
+                            int64_t color_stride, anr_stream_t stream);
+int anr_ingp_field_bwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                            const void* packed, const void* enc, int64_t enc_stride,
+                            const float* dirs, int64_t n_per_ray, int64_t M,
+                            const int32_t* rows, const float* d_sigma, const float* d_color,
+                            int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
+                            float* g_pos, float* g_dir, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Occupancy-grid sample culling (beyond the reference: BASELINE configs[4], SURVEY §8
+ * f3; csrc/occupancy.hip). occ: gx*gy*gz bytes (x fastest), nonzero = occupied, over the
+ * hash-grid domain [0,1] x [0,1] x [0, 1/zmul]. coords (M,3) f32 ray-major.
+ * anr_occupancy_count writes counts[anr_occupancy_n_blocks(M)] (int32, kept samples per
+ * block of 1024); the caller forms offsets = exclusive scan (int64) and the total K;
+ * anr_occupancy_compact writes rows (K,) int32 (kept sample indices, ascending) and
+ * coords_out (K,3). ------------------------------------------------------------------ */
+int64_t anr_occupancy_n_blocks(int64_t M);
+int anr_occupancy_count(const float* coords, int64_t M, const uint8_t* occ, int32_t gx,
+                        int32_t gy, int32_t gz, float zmul, int32_t* counts,
+                        anr_stream_t stream);
+int anr_occupancy_compact(const float* coords, int64_t M, const uint8_t* occ, int32_t gx,
+                          int32_t gy, int32_t gz, float zmul, const int64_t* offsets,
+                          int32_t* rows, float* coords_out, anr_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * NeRF path (configs/nerf.json): positional encoding (encoders.py:4-28) and the
  * hierarchical pdf sampler (samplers.py:50-103), forward and backward.

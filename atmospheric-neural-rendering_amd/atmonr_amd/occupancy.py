@@ -85,6 +85,11 @@ class OccupancyGrid:
         self.occ = (self.density > thr).to(torch.uint8)
         self.cell_fraction = float(self.occ.float().mean())  # one host read per update
 
+    def set_occupancy(self, occ: torch.Tensor) -> None:
+        """Install an occupancy mask (gx*gy*gz, x fastest; nonzero = occupied)."""
+        self.occ = (occ.reshape(-1) != 0).to(torch.uint8).to(self.device)
+        self.cell_fraction = float(self.occ.float().mean())
+
     def occupancy_fraction(self) -> float:
         return float(self.occ.float().mean())
 

@@ -216,8 +216,12 @@ struct Args {
   const int32_t* rows;
 };
 
+// ROWS is a compile-time choice: a run-time test on a.rows in the prefetch paths put a
+// branch join (and with it a wait for the in-flight loads) in front of the MFMAs
+template <bool ROWS>
 __device__ __forceinline__ int64_t dense_row(const Args& a, int64_t row) {
-  return a.rows ? static_cast<int64_t>(a.rows[row]) : row;
+  if constexpr (ROWS) return static_cast<int64_t>(a.rows[row]);
+  return row;
 }
 
 __device__ __forceinline__ h8 cat(h4 a, h4 b) {
@@ -253,6 +257,7 @@ struct Rows {
   float ds;       // dL/dsigma[row] (backward, g == 0 lanes)
 };
 
+template <bool ROWS>
 __device__ __forceinline__ void load_rows(const Args& a, int64_t row, int g, bool bwd, Rows& in) {
   in.xe = h8{};
   in.dx = in.dy = in.dz = 0.0f;
@@ -260,7 +265,7 @@ __device__ __forceinline__ void load_rows(const Args& a, int64_t row, int g, boo
   in.ds = 0.0f;
   if (row >= a.M) return;
   in.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
-  const int64_t drow = dense_row(a, row);
+  const int64_t drow = dense_row<ROWS>(a, row);
   if (g == 0) {
     const uint32_t ray = static_cast<uint32_t>(drow) / a.n_per_ray;
     const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
@@ -441,9 +446,10 @@ struct FwdRaw {
   float d0, d1, d2;
 };
 
+template <bool ROWS>
 __device__ __forceinline__ void load_fwd_raw(const Args& a, int64_t row, int g, FwdRaw& r) {
   r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
-  const uint32_t ray = static_cast<uint32_t>(dense_row(a, row)) / a.n_per_ray;
+  const uint32_t ray = static_cast<uint32_t>(dense_row<ROWS>(a, row)) / a.n_per_ray;
   const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
   r.d0 = d[0];
   r.d1 = d[1];
@@ -459,7 +465,7 @@ __device__ __forceinline__ void fwd_raw_to_rows(const FwdRaw& r, Rows& in) {
   in.ds = 0.0f;
 }
 
-template <int W, int NHD>
+template <int W, int NHD, bool ROWS>
 __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   // wave index through readfirstlane: the tile loop then runs on scalar registers
@@ -475,7 +481,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
     const bool valid = row < a.M;
     tile_forward<W, NHD, 1>(fw, &cur, &valid, g, &t, NoSink{});
     if (row < a.M) {
-      const int64_t drow = dense_row(a, row);
+      const int64_t drow = dense_row<ROWS>(a, row);
       if (g == 0) a.sigma[drow] = fmaxf(t.po[0], 0.0f);
       const int c0 = 4 * g;
       if (c0 + 3 < a.n_out && (a.color_stride & 3) == 0) {
@@ -493,17 +499,17 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   // full tiles: the next tile's inputs are in flight while this one computes (the
   // prefetch index is clamped, so the loop body has no branch around the loads)
   FwdRaw nraw;
-  if (tile < n_full) load_fwd_raw(a, tile * 16 + li, g, nraw);
+  if (tile < n_full) load_fwd_raw<ROWS>(a, tile * 16 + li, g, nraw);
   for (; tile < n_full; tile += tstride) {
     Rows cur;
     fwd_raw_to_rows(nraw, cur);
     const int64_t tn = tile + tstride < n_full ? tile + tstride : tile;
-    load_fwd_raw(a, tn * 16 + li, g, nraw);
+    load_fwd_raw<ROWS>(a, tn * 16 + li, g, nraw);
     body(cur, tile * 16 + li);
   }
   for (; tile < n_tiles; tile += tstride) {  // the last, partial tile
     Rows cur;
-    load_rows(a, tile * 16 + li, g, false, cur);
+    load_rows<ROWS>(a, tile * 16 + li, g, false, cur);
     body(cur, tile * 16 + li);
   }
 }
@@ -538,20 +544,21 @@ __device__ __forceinline__ void st4g(_Float16* base, int ld, int mrow, int col, 
 // Rows of the backward's wavefront w: tiles [w*tpw, (w+1)*tpw) of 32 rows. The f16
 // gradient scale of a wavefront is set from max(|dL/dcolor|, |dL/dsigma|) over its rows,
 // which this kernel computes first (one block per wavefront range, full occupancy).
+template <bool ROWS>
 __global__ void __launch_bounds__(256) absmax_kernel(Args a, int64_t rows_per_wave, float* wmax) {
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_wave;
   const int64_t r1 = r0 + rows_per_wave < a.M ? r0 + rows_per_wave : a.M;
   float m = 0.0f;
   if (a.n_out == 4 && (a.d_color_stride & 3) == 0) {
     for (int64_t rr = r0 + threadIdx.x; rr < r1; rr += blockDim.x) {
-      const int64_t r = dense_row(a, rr);
+      const int64_t r = dense_row<ROWS>(a, rr);
       const f4 d = *reinterpret_cast<const f4*>(a.d_color + r * a.d_color_stride);
       m = fmaxf(m, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
       if (a.d_sigma) m = fmaxf(m, fabsf(a.d_sigma[r]));
     }
   } else {
     for (int64_t rr = r0 + threadIdx.x; rr < r1; rr += blockDim.x) {
-      const int64_t r = dense_row(a, rr);
+      const int64_t r = dense_row<ROWS>(a, rr);
       for (int c = 0; c < a.n_out; ++c) m = fmaxf(m, fabsf(a.d_color[r * a.d_color_stride + c]));
       if (a.d_sigma) m = fmaxf(m, fabsf(a.d_sigma[r]));
     }
@@ -578,9 +585,10 @@ struct RawRows {
   f4 dc;
 };
 
+template <bool ROWS>
 __device__ __forceinline__ void load_raw(const Args& a, int64_t row, int g, RawRows& r) {
   r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
-  const int64_t drow = dense_row(a, row);
+  const int64_t drow = dense_row<ROWS>(a, row);
   const uint32_t ray = static_cast<uint32_t>(drow) / a.n_per_ray;
   const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
   r.d0 = d[0];
@@ -600,7 +608,7 @@ __device__ __forceinline__ void raw_to_rows(const RawRows& r, int g, Rows& in) {
   in.dc = g == 0 ? r.dc : z4;
 }
 
-template <int W, int NHD, bool FAST>
+template <int W, int NHD, bool FAST, bool ROWS>
 __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t tpw,
                                                   const float* wmax) {
   using N = Net<W, NHD>;
@@ -665,7 +673,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
   if constexpr (FAST) {
     if (t_begin < t_full_end) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_raw(a, t_begin * 32 + mt * 16 + li, g, nraw[mt]);
+      for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, t_begin * 32 + mt * 16 + li, g, nraw[mt]);
     }
   }
 #ifdef FIELD_STAMP
@@ -692,10 +700,10 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       for (int mt = 0; mt < 2; ++mt) raw_to_rows(nraw[mt], g, cur[mt]);
       const int64_t tn = tile + 1 < t_full_end ? tile + 1 : tile;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_raw(a, tn * 32 + mt * 16 + li, g, nraw[mt]);
+      for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, tn * 32 + mt * 16 + li, g, nraw[mt]);
     } else {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_rows(a, tile * 32 + mt * 16 + li, g, true, cur[mt]);
+      for (int mt = 0; mt < 2; ++mt) load_rows<ROWS>(a, tile * 32 + mt * 16 + li, g, true, cur[mt]);
     }
     const bool full = FULL;
     STAMP(0);
@@ -945,7 +953,7 @@ static int run(int op, const Args& a, hipStream_t st) {
   const int waves = 4;
   if (op == 1) {
     const int64_t tiles = (a.M + 15) / 16;
-    const void* fn = reinterpret_cast<const void*>(&fwd_kernel<W, NHD>);
+    const void* fn = reinterpret_cast<const void*>(&fwd_kernel<W, NHD, false>);
     static int pc = 0;
     if (pc == 0) {
       int nb = 0;
@@ -955,14 +963,17 @@ static int run(int op, const Args& a, hipStream_t st) {
     int64_t blocks = (tiles + waves - 1) / waves;
     if (blocks > 256LL * pc) blocks = 256LL * pc;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((fwd_kernel<W, NHD>), dim3(blocks), dim3(64 * waves), 0, st, a);
+    if (a.rows)
+      hipLaunchKernelGGL((fwd_kernel<W, NHD, true>), dim3(blocks), dim3(64 * waves), 0, st, a);
+    else
+      hipLaunchKernelGGL((fwd_kernel<W, NHD, false>), dim3(blocks), dim3(64 * waves), 0, st, a);
     return 0;
   }
   const bool fast = a.n_out == 4 && (a.d_color_stride & 3) == 0 && a.d_sigma != nullptr;
   const size_t lds = (static_cast<size_t>(N::n_packed) + waves * N::wave_lds) * 2;  // static
   if (lds > 160 * 1024) return 1;
-  const void* fn = fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true>)
-                        : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false>);
+  const void* fn = fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true, false>)
+                        : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false, false>);
   static int pc = 0;
   if (pc == 0) {
     int nb = 0;
@@ -983,12 +994,21 @@ static int run(int op, const Args& a, hipStream_t st) {
     if (hipMalloc(&g_wmax, nw * sizeof(float)) != hipSuccess) return 2;
     g_wmax_n = nw;
   }
-  hipLaunchKernelGGL(absmax_kernel, dim3(nw), dim3(256), 0, st, a, tpw * 32, g_wmax);
   const float target = ldexpf(1.0f, g_target_log2);
-  if (fast)
-    hipLaunchKernelGGL((bwd_kernel<W, NHD, true>), dim3(blocks), dim3(64 * waves), 0, st, a, target, tpw, g_wmax);
-  else
-    hipLaunchKernelGGL((bwd_kernel<W, NHD, false>), dim3(blocks), dim3(64 * waves), 0, st, a, target, tpw, g_wmax);
+  const dim3 grid(static_cast<unsigned>(blocks)), block(64 * waves);
+  if (a.rows) {
+    hipLaunchKernelGGL(absmax_kernel<true>, dim3(nw), dim3(256), 0, st, a, tpw * 32, g_wmax);
+    if (fast)
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, true>), grid, block, 0, st, a, target, tpw, g_wmax);
+    else
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, true>), grid, block, 0, st, a, target, tpw, g_wmax);
+  } else {
+    hipLaunchKernelGGL(absmax_kernel<false>, dim3(nw), dim3(256), 0, st, a, tpw * 32, g_wmax);
+    if (fast)
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, false>), grid, block, 0, st, a, target, tpw, g_wmax);
+    else
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, false>), grid, block, 0, st, a, target, tpw, g_wmax);
+  }
   return 0;
 }
 

@@ -33,8 +33,8 @@ def test_compact_matches_torch(dev, M, fill):
 
     g = torch.Generator().manual_seed(M)
     res = (16, 12, 8)
-    grid = OccupancyGrid(res, alt_compress=8.0, warmup=0, device=dev)
-    grid.occ = (torch.rand(16 * 12 * 8, generator=g) < fill).to(torch.uint8).to(dev)
+    grid = OccupancyGrid(res, alt_compress=8.0, warmup=0, max_fraction=1.0, device=dev)
+    grid.set_occupancy(torch.rand(16 * 12 * 8, generator=g) < fill)
     x = torch.rand(M, 3, generator=g)
     x[:, 2] /= 8.0
     x[:7] = torch.tensor([0.0, 1.0, 1.0 / 8.0]).expand(7, 3) if M >= 7 else x[:7]
@@ -67,12 +67,14 @@ def test_all_occupied_equals_uniform(scene, dev):
     from atmonr_amd.occupancy import OccupancyGrid
 
     a = _pipe(scene, dev)
-    b = _pipe(scene, dev, OccupancyGrid(warmup=0, update_every=10 ** 9, device=dev))
+    # max_fraction 1.0: the compacted (row-indirect) path runs although nothing is culled
+    b = _pipe(scene, dev, OccupancyGrid(warmup=0, update_every=10 ** 9, max_fraction=1.0,
+                                        device=dev))
     b.load_state_dict(a.state_dict())
     batch = next(iter(BatchLoader(scene, 512, seed=1)))
     u = torch.rand(512, 64, device=dev)
     ra, rb = a.forward(batch, u=u), b.forward(batch, u=u)
-    assert b.occupancy.last_fraction == 1.0
+    assert b.occupancy.active and b.occupancy.last_fraction == 1.0
     for k in ("color_map_fine", "color_map_atmo", "color_map_surf", "sigma_fine"):
         assert (ra[k] - rb[k]).abs().max() <= 1e-6 * ra[k].abs().max() + 1e-12, k
     a.compute_loss(batch, ra).backward()
@@ -88,8 +90,7 @@ def test_culled_samples_zero_kept_samples_exact(scene, dev):
 
     a = _pipe(scene, dev)
     occ = OccupancyGrid((32, 32, 8), warmup=0, update_every=10 ** 9, device=dev)
-    occ.occ = (torch.rand(32 * 32 * 8, generator=torch.Generator().manual_seed(3)) < 0.4
-               ).to(torch.uint8).to(dev)
+    occ.set_occupancy(torch.rand(32 * 32 * 8, generator=torch.Generator().manual_seed(3)) < 0.4)
     b = _pipe(scene, dev, occ)
     b.load_state_dict(a.state_dict())
     batch = next(iter(BatchLoader(scene, 256, seed=2)))
@@ -124,7 +125,7 @@ def test_training_with_grid_updates(scene, dev):
             opt.step()
             losses.append(loss.item())
             fracs.append(occ.last_fraction)
-    assert occ.steps == len(losses) and occ.active
+    assert occ.steps == len(losses) and occ.steps >= occ.warmup
     assert all(torch.isfinite(torch.tensor(losses)))
     assert sum(losses[-5:]) / 5 < 0.7 * sum(losses[:3]) / 3
     assert min(fracs) <= 1.0

@@ -27,10 +27,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAGS = {
     "hash_fwd": "hashgrid_fwd_kernel<3, 2, __half, __half>",
     "hash_bwd": "hashgrid_bwd_v2_kernel<3, float>",
-    "field_fwd": "field::fwd_kernel<64, 2>",
-    "field_bwd": "field::bwd_kernel<64, 2, true>",
-    "composite_fwd": "rb::fwd_kernel<float, 16, 1>",
-    "composite_bwd": "rb::bwd_kernel<float, 16, 1>",
+    "field_fwd": "field::fwd_kernel<64, 2, false>",
+    "field_bwd": "field::bwd_kernel<64, 2, true, false>",
+    "composite_fwd": "rb::fwd_kernel<float, 4, 1, 4>",
+    "composite_bwd": "rb::bwd_kernel<float, 4, 1, 4>",
     "sampler": "sample_uniform_bins_kernel",
 }
 

@@ -171,6 +171,14 @@ _SIGNATURES = {
             c_int64, _P, c_int32, c_int64, _P, _P,
         ],
     ),
+    "anr_mlp_bwd_workspace_bytes": (c_int64, [POINTER(MlpDesc), c_int64]),
+    "anr_mlp_bwd_ws": (
+        c_int32,
+        [
+            POINTER(MlpDesc), c_int32, _P, _P, c_int32, c_int64, c_int64, _P, c_int32,
+            c_int64, _P, c_int32, c_int64, _P, _P, c_int64, _P,
+        ],
+    ),
     "anr_ingp_dir_mlp_fwd": (
         c_int32,
         [POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64, _P, c_int32,

@@ -262,10 +262,15 @@ class _NetworkFn(torch.autograd.Function):
         din = None
         if ctx.needs_input_grad[0]:
             din = torch.empty(x.shape, device=x.device, dtype=x.dtype)
-        call("anr_mlp_bwd", ctypes.byref(net.desc), prec, ptr(p), ptr(x), dtype_code(x.dtype),
-             x.stride(0), x.shape[0], ptr(dout), dtype_code(dout.dtype), dout.stride(0),
-             ptr(din), dtype_code(x.dtype), x.stride(0) if din is not None else 0,
-             ptr(dparams), _lib.stream(x.device))
+        # small batches: per-wavefront dW rows + a fixed-order sum instead of atomics
+        ws_bytes = net.bwd_workspace_bytes(x.shape[0])
+        ws = (torch.empty(ws_bytes // 4, device=x.device, dtype=torch.float32)
+              if ws_bytes else None)
+        call("anr_mlp_bwd_ws", ctypes.byref(net.desc), prec, ptr(p), ptr(x),
+             dtype_code(x.dtype), x.stride(0), x.shape[0], ptr(dout), dtype_code(dout.dtype),
+             dout.stride(0), ptr(din), dtype_code(x.dtype),
+             x.stride(0) if din is not None else 0, ptr(dparams), ptr(ws), ws_bytes,
+             _lib.stream(x.device))
         return din, None if direct else dparams, None
 
 
@@ -303,6 +308,13 @@ class Network(nn.Module):
             bound = math.sqrt(6.0 / (o + i))
             chunks.append((torch.rand(o * i, generator=gen) * 2 - 1) * bound)
         self.params = nn.Parameter(torch.cat(chunks).float(), requires_grad=True)
+
+    def bwd_workspace_bytes(self, M: int) -> int:
+        """Scratch bytes the backward can use at batch M (anr_mlp_bwd_workspace_bytes)."""
+        cache = self.__dict__.setdefault("_ws_bytes", {})
+        if M not in cache:
+            cache[M] = int(_lib.load().anr_mlp_bwd_workspace_bytes(ctypes.byref(self.desc), M))
+        return cache[M]
 
     def layer(self, k: int) -> torch.Tensor:
         """View of layer k's (out, in) weight matrix inside the flat params."""

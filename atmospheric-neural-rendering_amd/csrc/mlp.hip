@@ -405,7 +405,9 @@ constexpr size_t kLdsBudget = 160 * 1024;
 int mlp_fused_try(const anr_mlp_desc* d, int32_t precision, bool bwd, const void* params,
                   const void* in, int32_t in_dt, int64_t in_stride, int64_t M,
                   const void* dout, int32_t dout_dt, int64_t dout_stride, void* out,
-                  int32_t out_dt, int64_t out_stride, float* dparams, hipStream_t st);
+                  int32_t out_dt, int64_t out_stride, float* dparams, hipStream_t st,
+                  float* slab = nullptr, int64_t slab_floats = 0);
+bool mlp_fused_has(const anr_mlp_desc* d);
 
 // ANR_MLP_GENERIC=1 (or anr_mlp_force_generic) forces the generic kernels.
 static int g_force_generic = [] {
@@ -476,11 +478,23 @@ extern "C" int anr_mlp_fwd(const anr_mlp_desc* d, int32_t precision, const void*
   return ANR_OK;
 }
 
-extern "C" int anr_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void* params,
-                           const void* in, int32_t in_dtype, int64_t in_stride, int64_t M,
-                           const void* dout, int32_t dout_dtype, int64_t dout_stride,
-                           void* din, int32_t din_dtype, int64_t din_stride, float* dparams,
-                           anr_stream_t stream) {
+// Batches up to this many rows may use the slab (per-wavefront dW rows + one reduction)
+// instead of atomics in the specialised backward: with one 16-row tile per wavefront the
+// atomics pile onto the same few KB of dW (the per-ray surface network, 8192 rows).
+constexpr int64_t kSlabMaxRows = 1 << 16;
+
+extern "C" int64_t anr_mlp_bwd_workspace_bytes(const anr_mlp_desc* d, int64_t M) {
+  using namespace anr;
+  if (check_desc(d) != ANR_OK || M <= 0 || M > kSlabMaxRows || !mlp_fused_has(d)) return 0;
+  const int64_t waves = (M + 15) / 16 + 3;  // one 16-row tile per wavefront, 4 per block
+  return waves * n_params_of(d) * static_cast<int64_t>(sizeof(float));
+}
+
+static int mlp_bwd_impl(const anr_mlp_desc* d, int32_t precision, const void* params,
+                        const void* in, int32_t in_dtype, int64_t in_stride, int64_t M,
+                        const void* dout, int32_t dout_dtype, int64_t dout_stride, void* din,
+                        int32_t din_dtype, int64_t din_stride, float* dparams,
+                        void* workspace, int64_t workspace_bytes, anr_stream_t stream) {
   using namespace anr;
   if (int rc = check_desc(d)) return rc;
   if (M == 0) return ANR_OK;
@@ -492,7 +506,9 @@ extern "C" int anr_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void*
   if (M == 0) return ANR_OK;
   if (!force_generic() &&
       mlp_fused_try(d, precision, true, params, in, in_dtype, in_stride, M, dout, dout_dtype,
-                    dout_stride, din, din_dtype, din_stride, dparams, as_stream(stream)) == 0) {
+                    dout_stride, din, din_dtype, din_stride, dparams, as_stream(stream),
+                    M <= kSlabMaxRows ? static_cast<float*>(workspace) : nullptr,
+                    workspace_bytes / static_cast<int64_t>(sizeof(float))) == 0) {
     ANR_CHECK_LAUNCH("anr_mlp_bwd(fused)");
     return ANR_OK;
   }
@@ -538,4 +554,23 @@ extern "C" int anr_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void*
   }
   ANR_CHECK_LAUNCH("anr_mlp_bwd");
   return ANR_OK;
+}
+
+extern "C" int anr_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void* params,
+                           const void* in, int32_t in_dtype, int64_t in_stride, int64_t M,
+                           const void* dout, int32_t dout_dtype, int64_t dout_stride,
+                           void* din, int32_t din_dtype, int64_t din_stride, float* dparams,
+                           anr_stream_t stream) {
+  return mlp_bwd_impl(d, precision, params, in, in_dtype, in_stride, M, dout, dout_dtype,
+                      dout_stride, din, din_dtype, din_stride, dparams, nullptr, 0, stream);
+}
+
+extern "C" int anr_mlp_bwd_ws(const anr_mlp_desc* d, int32_t precision, const void* params,
+                              const void* in, int32_t in_dtype, int64_t in_stride, int64_t M,
+                              const void* dout, int32_t dout_dtype, int64_t dout_stride,
+                              void* din, int32_t din_dtype, int64_t din_stride, float* dparams,
+                              void* workspace, int64_t workspace_bytes, anr_stream_t stream) {
+  return mlp_bwd_impl(d, precision, params, in, in_dtype, in_stride, M, dout, dout_dtype,
+                      dout_stride, din, din_dtype, din_stride, dparams, workspace,
+                      workspace_bytes, stream);
 }

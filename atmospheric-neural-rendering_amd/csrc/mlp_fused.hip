@@ -117,7 +117,34 @@ struct Args {
   const float* dirs;
   int64_t n_per_ray;
   const float* d_sigma;
+  // bwd (nullable): one n_params row of f32 per wavefront; each wavefront stores its dW
+  // there instead of adding it with atomics, and slab_reduce_kernel sums the rows into
+  // dparams (small batches: the atomics would pile onto the same few KB)
+  float* slab;
+  int64_t slab_floats;
 };
+
+// dparams[p] += sum over the nw slab rows of slab[w * n + p]. Block = 64 params x 16 row
+// groups: group y sums rows y, y+16, ... and the 16 partials are added in a fixed order
+// (deterministic; 16 independent load streams per column instead of one serial walk).
+__global__ void __launch_bounds__(1024) slab_reduce_kernel(const float* __restrict__ slab,
+                                                           int64_t nw, int64_t n,
+                                                           float* __restrict__ dparams) {
+  __shared__ float part[16][64];
+  const int x = threadIdx.x & 63, y = threadIdx.x >> 6;
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * 64 + x;
+  float acc = 0.0f;
+  if (p < n)
+    for (int64_t w = y; w < nw; w += 16) acc += slab[w * n + p];
+  part[y][x] = acc;
+  __syncthreads();
+  if (y == 0 && p < n) {
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += part[j][x];
+    dparams[p] += s;
+  }
+}
 
 // Compile-time network shape.
 template <int W, int NIP, int NOP, int NH>
@@ -541,7 +568,12 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = mt * 16 + 4 * (lane >> 4) + i, col = nt * 16 + (lane & 15);
-          if (d[i] != 0.0f) atomicAdd(a.dparams + S::woff(k) + row * K + col, d[i] * inv_s);
+          if (a.slab) {
+            const int64_t w_id = static_cast<int64_t>(blockIdx.x) * waves + wave;
+            a.slab[w_id * S::n_params + S::woff(k) + row * K + col] = d[i] * inv_s;
+          } else if (d[i] != 0.0f) {
+            atomicAdd(a.dparams + S::woff(k) + row * K + col, d[i] * inv_s);
+          }
         }
       }
   }
@@ -590,9 +622,17 @@ static int launch(bool bwd, const Args& a, hipStream_t st) {
     const int64_t by_tiles = (tiles + waves * min_tiles - 1) / (waves * min_tiles);
     if (blocks > by_tiles) blocks = by_tiles > 0 ? by_tiles : 1;
   }
-  if (bwd)
+  if (bwd) {
+    Args b = a;
+    if (a.slab && blocks * waves * static_cast<int64_t>(S::n_params) > a.slab_floats)
+      b.slab = nullptr;  // workspace too small for this grid: atomics
     hipLaunchKernelGGL((bwd_kernel<TC, W, NIP, NOP, NH, MODE>), dim3(blocks), dim3(64 * waves),
-                       lds, st, a);
+                       lds, st, b);
+    if (b.slab)
+      hipLaunchKernelGGL(slab_reduce_kernel, dim3(static_cast<unsigned>((S::n_params + 63) / 64)),
+                         dim3(1024), 0, st, b.slab, blocks * waves,
+                         static_cast<int64_t>(S::n_params), a.dparams);
+  }
   else
     hipLaunchKernelGGL((fwd_kernel<TC, W, NIP, NOP, NH, MODE>), dim3(blocks), dim3(64 * waves),
                        lds, st, a);
@@ -627,13 +667,23 @@ static int dispatch_dir(const anr_mlp_desc* d, bool bwd, const Args& a, hipStrea
 
 }  // namespace fused
 
+// True if dispatch_tc has a specialised kernel for this shape (the plain MLP entry points).
+bool mlp_fused_has(const anr_mlp_desc* d) {
+  return d->n_output_padded == 16 && (d->width == 32 || d->width == 64) &&
+         (d->n_hidden_layers == 1 || d->n_hidden_layers == 2) &&
+         (d->n_input_padded == 16 || d->n_input_padded == 32 || d->n_input_padded == 48);
+}
+
 // Returns 0 if a specialised kernel was launched, 1 if the caller must use the generic
 // kernel. The weights must already be in compute precision.
 int mlp_fused_try(const anr_mlp_desc* d, int32_t precision, bool bwd, const void* params,
                   const void* in, int32_t in_dt, int64_t in_stride, int64_t M,
                   const void* dout, int32_t dout_dt, int64_t dout_stride, void* out,
-                  int32_t out_dt, int64_t out_stride, float* dparams, hipStream_t st) {
+                  int32_t out_dt, int64_t out_stride, float* dparams, hipStream_t st,
+                  float* slab, int64_t slab_floats) {
   fused::Args a{};
+  a.slab = slab;
+  a.slab_floats = slab_floats;
   a.n_in = d->n_input;
   a.n_out = d->n_output;
   a.out_relu = d->output_activation == ANR_ACT_RELU;

@@ -208,6 +208,18 @@ int anr_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void* params,
                 const void* dout, int32_t dout_dtype, int64_t dout_stride, void* din,
                 int32_t din_dtype, int64_t din_stride, float* dparams,
                 anr_stream_t stream);
+/* Scratch bytes anr_mlp_bwd_ws can use for M rows (0: it would not use any). With it the
+ * specialised backward stores one dW row per wavefront and sums them in a fixed order
+ * instead of adding with float atomics (small batches, e.g. the per-ray surface
+ * network: deterministic and without the atomics' contention). */
+int64_t anr_mlp_bwd_workspace_bytes(const anr_mlp_desc* d, int64_t M);
+/* anr_mlp_bwd with a device workspace (f32-aligned, workspace_bytes long; may be null or
+ * smaller than anr_mlp_bwd_workspace_bytes, then the atomics path runs). */
+int anr_mlp_bwd_ws(const anr_mlp_desc* d, int32_t precision, const void* params,
+                   const void* in, int32_t in_dtype, int64_t in_stride, int64_t M,
+                   const void* dout, int32_t dout_dtype, int64_t dout_stride, void* din,
+                   int32_t din_dtype, int64_t din_stride, float* dparams, void* workspace,
+                   int64_t workspace_bytes, anr_stream_t stream);
 
 /* Instant-NGP dir MLP with the dir encoding fused into its input
  * (instant_ngp.py:165-171): row r of the network input is

@@ -76,3 +76,9 @@ def test_mlp_param_counts():
                                       (36, 4, 64, 2, 64 * 48 + 64 * 64 + 16 * 64)]:
         d = _lib.mlp_desc(n_in, n_out, w, h, False)
         assert lib.anr_mlp_n_params(ctypes.byref(d)) == expect
+        # backward workspace: one dW row per wavefront (16-row tiles, 4 per block), only
+        # for batches up to 64Ki rows
+        nw = (8192 + 15) // 16 + 3
+        assert lib.anr_mlp_bwd_workspace_bytes(ctypes.byref(d), 8192) == 4 * nw * expect
+        assert lib.anr_mlp_bwd_workspace_bytes(ctypes.byref(d), 1 << 17) == 0
+        assert lib.anr_mlp_bwd_workspace_bytes(ctypes.byref(d), 0) == 0

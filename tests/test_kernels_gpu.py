@@ -296,6 +296,50 @@ def test_mlp_fwd_bwd(dev, mlp_path, n_in, n_out, width, n_hidden, out_relu, half
     close(dparams, pr.grad, rel=rel * 2, atol=1e-8)
 
 
+@pytest.mark.parametrize("n_in,n_out,width,n_hidden,out_relu", MLP_CASES)
+@pytest.mark.parametrize("M", [8192, 1001, 16])
+def test_mlp_bwd_workspace(dev, n_in, n_out, width, n_hidden, out_relu, M):
+    """anr_mlp_bwd_ws: the slab path (per-wavefront dW rows, fixed-order sum) gives the
+    atomics path's dparams (accumulated into, not overwritten), is bit-reproducible, and a
+    too-small workspace falls back to the atomics."""
+    from atmonr_amd import _lib
+
+    lib = _lib.load()
+    d = _lib.mlp_desc(n_in, n_out, width, n_hidden, out_relu)
+    nparam = lib.anr_mlp_n_params(ctypes.byref(d))
+    ws_bytes = lib.anr_mlp_bwd_workspace_bytes(ctypes.byref(d), M)
+    specialised = n_out <= 16 and width in (32, 64) and n_hidden in (1, 2)
+    assert (ws_bytes > 0) == specialised and ws_bytes % 4 == 0
+    if not specialised:  # generic kernel: atomics only, no workspace
+        return
+    gen = torch.Generator().manual_seed(M + width)
+    pd = (torch.randn(nparam, generator=gen) * (1.0 / width) ** 0.5).to(dev).half()
+    xd = torch.randn(M, n_in, generator=gen).to(dev).half()
+    dd = (torch.randn(M, n_out, generator=gen) * 1e-3).to(dev)
+    base = torch.randn(nparam, generator=gen).to(dev) * 1e-3
+    s = _lib.stream(dev)
+
+    def run(ws, nbytes):
+        dp = base.clone()
+        din = torch.empty(M, n_in, device=dev)
+        _lib.call("anr_mlp_bwd_ws", ctypes.byref(d), _lib.F16, pd.data_ptr(), xd.data_ptr(),
+                  _lib.F16, n_in, M, dd.data_ptr(), _lib.F32, n_out, din.data_ptr(), _lib.F32,
+                  n_in, dp.data_ptr(), _lib.ptr(ws), nbytes, s)
+        return dp, din
+
+    ws = torch.full((ws_bytes // 4,), float("nan"), device=dev)  # every slot is written
+    dp_a, din_a = run(None, 0)
+    dp_s, din_s = run(ws, ws_bytes)
+    dp_s2, _ = run(ws, ws_bytes)
+    dp_small, _ = run(ws, 4 * nparam - 4)
+    assert torch.equal(din_a, din_s)
+    assert torch.equal(dp_s, dp_s2)
+    g = dp_a - base
+    assert ((dp_s - base - g).norm() / g.norm()).item() <= 1e-5
+    assert ((dp_small - base - g).norm() / g.norm()).item() <= 1e-5
+    assert lib.anr_mlp_bwd_workspace_bytes(ctypes.byref(d), 1 << 20) == 0
+
+
 # ------------------------------------------------------------------ K8
 @pytest.fixture(params=["blocked", "generic"])
 def comp_path(request):

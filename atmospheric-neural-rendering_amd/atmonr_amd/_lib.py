@@ -367,6 +367,26 @@ def grad_target(param: torch.nn.Parameter, dev) -> tuple[torch.Tensor, bool]:
     return torch.zeros(param.shape, device=dev, dtype=torch.float32), False
 
 
+def grad_use(*params) -> None:
+    """A forward that will accumulate these params' gradients directly (grad_target) is
+    about to run with autograd recording: counted by an overlapping FlatGradBucket."""
+    if not torch.is_grad_enabled():
+        return
+    for p in params:
+        b = getattr(p, "_anr_bucket", None)
+        if b is not None and p.requires_grad:
+            b.grad_use(p)
+
+
+def grad_done(*params) -> None:
+    """The backward kernel that finishes these params' (direct) gradients for one use has
+    been launched: an overlapping FlatGradBucket may issue the chunk's all-reduce."""
+    for p in params:
+        b = getattr(p, "_anr_bucket", None)
+        if b is not None:
+            b.grad_done(p)
+
+
 def compute_copy(param: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """``param.detach().to(dtype)`` without a conversion pass per forward.
 

@@ -37,6 +37,13 @@ from ._lib import call, dtype_code, ptr
 _grad_target = _lib.grad_target
 
 
+def _done(*pairs) -> None:
+    """_lib.grad_done for each (direct, param) pair whose gradient was written directly."""
+    for direct, p in zip(pairs[::2], pairs[1::2]):
+        if direct:
+            _lib.grad_done(p)
+
+
 class IngpFieldFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, coords, dirs, n_per_ray: int, p_hash, p_pos, p_dir, pipe, rows=None,
@@ -135,6 +142,7 @@ class IngpFieldFn(torch.autograd.Function):
              tag="pos_mlp_bwd")
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
+        _done(direct_d, p_dir, direct_p, p_pos, direct_h, p_hash)
         return (None, None, None, None if direct_h else g_hash, None if direct_p else g_pos,
                 None if direct_d else g_dir, None, None, None)
 
@@ -165,8 +173,10 @@ class IngpFieldFn(torch.autograd.Function):
                  ptr(dirs), ctx.n_per_ray, M, ptr(ctx.rows), ptr(d_sigma), ptr(d_color),
                  d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), s,
                  tag="field_bwd")
+        _done(direct_p, p_pos, direct_d, p_dir)  # MLP grads final: their all-reduce may start
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
+        _done(direct_h, p_hash)
         return (None, None, None, None if direct_h else g_hash, None if direct_p else g_pos,
                 None if direct_d else g_dir, None, None, None)
 

@@ -8,6 +8,18 @@ the union batch. :class:`FlatGradBucket` makes every parameter's ``.grad`` a vie
 one contiguous f32 buffer, so backward accumulates in place and a step needs exactly
 one collective: ``all_reduce(AVG)`` of the whole buffer (RCCL over xGMI on MI355X;
 gloo on CPU for the tests).
+
+Overlap (``enable_overlap``): the buffer is cut into chunks along parameter boundaries and
+a chunk's all-reduce is issued (async, stream-ordered behind the kernel that finished its
+last gradient) as soon as every parameter in it is done for the step, so it runs while the
+rest of the backward computes. The Instant-NGP step produces the surface network's and
+the MLPs' gradients before the 3-D hash grid's (the last backward kernel): their
+all-reduce hides behind the hash-grid backward. Modules report uses and completions
+(``_lib.grad_use`` before a forward that will write a bucketed gradient directly,
+``_lib.grad_done`` after the backward kernel that wrote it); a parameter is done when its
+completions have caught up with its uses. ``all_reduce()`` issues whatever is left and
+waits for everything. Not for gradient accumulation over several backward passes per
+step (a chunk could be reduced before the later passes add to it).
 """
 
 from __future__ import annotations
@@ -48,9 +60,77 @@ class FlatGradBucket:
         zero_grad_in_step over all bucketed params): the next zero() needs no fill."""
         self._known_zero = True
 
+    # ------------------------------------------------------------------ overlap
+    def enable_overlap(self, min_chunk_bytes: int = 4 << 20, group=None) -> None:
+        """Issue each chunk's all-reduce as soon as its gradients are final (see module
+        doc). Chunks: consecutive parameters merged until ``min_chunk_bytes``."""
+        self._group = group
+        self._chunks = []  # (start, end, [param index])
+        start, idx = 0, []
+        off = 0
+        for i, p in enumerate(self.params):
+            idx.append(i)
+            off += p.numel()
+            if 4 * (off - start) >= min_chunk_bytes or i == len(self.params) - 1:
+                self._chunks.append((start, off, idx))
+                start, idx = off, []
+        self._chunk_of = {}
+        for c, (_, _, ids) in enumerate(self._chunks):
+            for i in ids:
+                self._chunk_of[id(self.params[i])] = c
+        for p in self.params:
+            p._anr_bucket = self
+        self._pending = {id(p): 0 for p in self.params}
+        self._works = [None] * len(self._chunks)
+        self.early_issued = 0  # chunks issued before all_reduce() in the last step
+        self._early = 0
+
+    @property
+    def overlap(self) -> bool:
+        return hasattr(self, "_chunks")
+
+    def _distributed(self, group=None) -> bool:
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+    def grad_use(self, p) -> None:
+        if self.overlap and id(p) in self._pending:
+            self._pending[id(p)] += 1
+
+    def grad_done(self, p) -> None:
+        if not self.overlap or id(p) not in self._pending:
+            return
+        self._pending[id(p)] -= 1
+        c = self._chunk_of[id(p)]
+        if self._works[c] is None and all(self._pending[id(self.params[i])] <= 0
+                                          for i in self._chunks[c][2]):
+            self._issue(c)
+            self._early += 1
+
+    def _issue(self, c) -> None:
+        s, e, _ = self._chunks[c]
+        if self._distributed(self._group):
+            self._works[c] = dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.AVG,
+                                             group=self._group, async_op=True)
+        else:
+            self._works[c] = True
+
     def all_reduce(self, group=None) -> None:
-        """Average the gradient over the ranks of ``group`` (no-op when not distributed)."""
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        """Average the gradient over the ranks of ``group`` (no-op when not distributed).
+        With overlap: issue the chunks not yet issued, then wait for all of them (stream
+        waits for RCCL, so the optimizer kernels queue behind the collectives)."""
+        if self.overlap:
+            for c in range(len(self._chunks)):
+                if self._works[c] is None:
+                    self._issue(c)
+            for w in self._works:
+                if w is not True and w is not None:
+                    w.wait()
+            self.early_issued = self._early
+            self._works = [None] * len(self._chunks)
+            self._pending = {k: 0 for k in self._pending}
+            self._early = 0
+            return
+        if self._distributed(group):
             dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=group)
 
     @property

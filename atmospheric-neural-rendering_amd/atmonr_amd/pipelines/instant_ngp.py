@@ -136,6 +136,7 @@ class InstantNGPPipeline(Pipeline):
         if occ is not None and self.training:
             occ.update(pipeline_density(self))
         params = (self.pos_encoder.params, self.pos_mlp.params, self.dir_mlp.params, self)
+        _lib.grad_use(*params[:3])  # IngpFieldFn accumulates these three directly
         if occ is not None and occ.active:
             # only samples in occupied cells reach the hash grid and the MLPs; sigma and
             # color come back dense (B*N rows) with zeros at the culled samples

@@ -193,6 +193,8 @@ class _EncodingFn(torch.autograd.Function):
             dps = dparams[poff:poff + leaf.n_params] if dparams is not None else None
             leaf.bwd(xs, p[poff:poff + leaf.n_params], dout, col_out, dps, dxs, s)
             col_out += leaf.n_out
+        if direct:
+            _lib.grad_done(enc.params)
         if dx is not None:
             dx = dx.to(x.dtype)
         return dx, None if direct else dparams, None
@@ -231,6 +233,7 @@ class Encoding(nn.Module):
         if x.dim() != 2 or x.shape[1] != self.n_input_dims:
             raise ANRError(f"Encoding expects (M, {self.n_input_dims}) input, got {tuple(x.shape)}")
         x = x.to(torch.float32).contiguous()
+        _lib.grad_use(self.params)
         return _EncodingFn.apply(x, self.params, self)
 
     def extra_repr(self) -> str:
@@ -271,6 +274,8 @@ class _NetworkFn(torch.autograd.Function):
              dout.stride(0), ptr(din), dtype_code(x.dtype),
              x.stride(0) if din is not None else 0, ptr(dparams), ptr(ws), ws_bytes,
              _lib.stream(x.device))
+        if direct:
+            _lib.grad_done(net.params)
         return din, None if direct else dparams, None
 
 
@@ -327,6 +332,7 @@ class Network(nn.Module):
             raise ANRError(f"Network expects (M, {self.n_input_dims}) input, got {tuple(x.shape)}")
         if x.dtype not in (torch.float16, torch.float32):
             x = x.float()
+        _lib.grad_use(self.params)
         return _NetworkFn.apply(x.contiguous(), self.params, self)
 
     def extra_repr(self) -> str:

@@ -73,3 +73,103 @@ def test_two_rank_sharding_and_grad_average():
     x = torch.tensor(b0 + b1, dtype=torch.float32)
     ((w[0] * x + w[1] - 1.0) ** 2).mean().backward()
     assert torch.allclose(torch.tensor(g0), w.grad, rtol=1e-6)
+
+
+def _overlap_worker(rank, world, port, out):
+    import sys
+
+    from tests.conftest import PKG
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from atmonr_amd import _lib
+    from atmonr_amd.parallel import FlatGradBucket
+
+    class Direct(torch.autograd.Function):
+        """y = x * p, accumulating dL/dp into p.grad itself (as the HIP modules do)."""
+
+        @staticmethod
+        def forward(ctx, x, p):
+            ctx.save_for_backward(x, p)
+            return x * p
+
+        @staticmethod
+        def backward(ctx, g):
+            x, p = ctx.saved_tensors
+            p.grad += (g * x).sum(0)
+            order.append(("done", p._tag))
+            _lib.grad_done(p)
+            order.append(("issued", sum(w is not None for w in bucket._works)))
+            return g * p, None
+
+    order = []
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.full((n,), 0.1 * (i + 1))) for i, n in
+          enumerate([4096, 3, 5, 2048])]
+    for i, p in enumerate(ps):
+        p._tag = i
+    bucket = FlatGradBucket(ps, device=torch.device("cpu"))
+    bucket.enable_overlap(min_chunk_bytes=4 * 1024)  # chunks: [p0], [p1, p2, p3]
+    grads, local = [], []
+    for step in range(2):
+        x = torch.randn(8, 4096, generator=torch.Generator().manual_seed(10 * step + rank))
+        # p0 feeds everything (its gradient is final last); p1..p3 act on the output
+        _lib.grad_use(ps[0])
+        h = Direct.apply(x, ps[0])
+        _lib.grad_use(ps[3])
+        a = Direct.apply(h[:, :2048], ps[3])
+        _lib.grad_use(ps[1])
+        b = Direct.apply(h[:, :3], ps[1])
+        _lib.grad_use(ps[2])
+        c = Direct.apply(h[:, :5], ps[2])
+        _lib.grad_use(ps[2])  # p2 used twice: final only after both backward uses
+        c2 = Direct.apply(h[:, 5:10], ps[2])
+        loss = (a ** 2).mean() + b.sum() + (c * c2).sum()
+        bucket.zero()
+        loss.backward()
+        issued_before = sum(w is not None for w in bucket._works)
+        bucket.all_reduce()
+        grads.append([p.grad.clone() for p in ps])
+        # this rank's own gradient, plain autograd
+        q = [p.detach().clone().requires_grad_(True) for p in ps]
+        hq = x * q[0]
+        ((hq[:, :2048] * q[3]) ** 2).mean().backward(retain_graph=True)
+        ((hq[:, :3] * q[1]).sum() + ((hq[:, :5] * q[2]) * (hq[:, 5:10] * q[2])).sum()).backward()
+        local.append([t.grad.clone() for t in q])
+        if step == 0:
+            out[f"order{rank}"] = list(order)
+            out[f"early{rank}"] = (issued_before, bucket.early_issued)
+        for p in ps:
+            p.grad.zero_()
+    out[rank] = [[g.tolist() for g in gs] for gs in grads]
+    out[f"local{rank}"] = [[g.tolist() for g in gs] for gs in local]
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_overlapped_bucket_matches_plain_all_reduce():
+    """enable_overlap: each chunk is all-reduced during the backward as soon as its
+    gradients are final (not while a param still owes a backward use), the chunk of the
+    first-used param last; the averaged gradients equal the ranks' own gradients
+    averaged."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_overlap_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        issued_before, early = out[f"early{r}"]
+        assert issued_before == 2 and early == 2  # both chunks issued inside backward
+        order = out[f"order{r}"]
+        # the chunk [p1, p2, p3] is issued right after its last completion, not before
+        dones = [i for i, e in enumerate(order) if e[0] == "done"]
+        first_issue = next(i for i, e in enumerate(order) if e[0] == "issued" and e[1] == 1)
+        finals = [order[i][1] for i in dones if i < first_issue]
+        assert sorted(set(finals)) == [1, 2, 3] and finals.count(2) == 2
+        assert order[-2] == ("done", 0) and order[-1] == ("issued", 2)  # [p0] last
+    g0, g1 = out[0], out[1]
+    assert g0 == g1
+    for step in range(2):
+        for k in range(4):
+            want = (torch.tensor(out["local0"][step][k]) + torch.tensor(out["local1"][step][k])) / 2
+            assert torch.allclose(torch.tensor(g0[step][k]), want, rtol=1e-5, atol=1e-7)

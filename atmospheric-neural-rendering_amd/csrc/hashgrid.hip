@@ -861,7 +861,10 @@ static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
   return true;
 }
 
-// v2: one chunk per wave; aim for >= 32K waves (8 per SIMD on 1024 SIMDs, x4 slack).
+// v2: one chunk per wave; aim for >= 32K waves (8 per SIMD on 1024 SIMDs, x4 slack) with
+// chunks of up to 256 samples: every chunk ends with a flush of all its corners, and at
+// the bench size (8.39 M samples, 32K waves) 256 beat 128 / 192 / 384 (hash bwd 1.27 ->
+// 1.17 ms in the timed region; profiles/r01_hash_bwd_chunk_sweep.log).
 static int64_t env_k(const char* name) {
   const char* e = getenv(name);  // profiling override of the chunk length
   return e ? atoll(e) : 0;
@@ -871,7 +874,7 @@ static int64_t pick_chunk_v2(int64_t M) {
   if (over > 0) return over;
   int64_t K = M / 32768;
   if (K < 1) K = 1;
-  if (K > 128) K = 128;
+  if (K > 256) K = 256;
   return K;
 }
 
@@ -900,13 +903,14 @@ static int fwd_lpw() {
 }
 
 // Samples per chunk: long chunks amortise the per-cell gathers/atomics, but the grid
-// must still fill 256 CUs. Aim for >= 64K chunks.
+// must still fill 256 CUs. Aim for >= 64K chunks (bench size: 128 samples per chunk,
+// forward 0.656 -> 0.646 ms against 64).
 static int64_t pick_chunk(int64_t M) {
   static const int64_t over = env_k("ANR_HASH_KF");
   if (over > 0) return over;
   int64_t K = M / 65536;
   if (K < 1) K = 1;
-  if (K > 64) K = 64;
+  if (K > 128) K = 128;
   return K;
 }
 

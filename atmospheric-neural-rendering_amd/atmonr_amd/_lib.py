@@ -387,6 +387,41 @@ def grad_done(*params) -> None:
             b.grad_done(p)
 
 
+_side_streams: dict = {}
+
+
+def side_stream(device) -> "torch.cuda.Stream":
+    """One extra HIP stream per device for work independent of the main per-sample chain
+    (the per-ray surface branch of InstantNGPPipeline)."""
+    key = torch.device(device).index
+    st = _side_streams.get(key)
+    if st is None:
+        st = _side_streams[key] = torch.cuda.Stream(device=device)
+    return st
+
+
+class JoinAtBackwardEnd(torch.autograd.Function):
+    """Identity on a tensor produced on a side stream. Its backward (which autograd runs
+    on that side stream, as the forward) queues an end-of-backward callback making the
+    caller's stream wait for the side stream: the branch's backward kernels write the
+    parameter gradients directly (grad_target), so autograd's own leaf-stream sync does
+    not cover them, and optimizer / gradient reads after ``backward()`` must see them."""
+
+    @staticmethod
+    def forward(ctx, x, main):
+        ctx.main = main
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        side = torch.cuda.current_stream(g.device)
+        g.record_stream(side)  # produced on the main stream, read here
+        main = ctx.main
+        torch.autograd.Variable._execution_engine.queue_callback(
+            lambda: main.wait_stream(side))
+        return g, None
+
+
 def compute_copy(param: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """``param.detach().to(dtype)`` without a conversion pass per forward.
 

@@ -17,6 +17,7 @@ Two execution paths, identical semantics:
 
 from __future__ import annotations
 
+import os
 from itertools import chain
 from typing import Any, Mapping
 
@@ -51,6 +52,7 @@ class InstantNGPPipeline(Pipeline):
             fused = False
         self.fused = fused
         self.dtype = dtype
+        self.surface_stream = os.environ.get("ANR_SURFACE_STREAM", "1") != "0"
         ingp = self.config["instant_ngp"]
         nb = self.config["num_bands"]
         fdt = torch.float32 if fused else None  # fused path keeps activations/grads in f32
@@ -128,9 +130,35 @@ class InstantNGPPipeline(Pipeline):
                   o.shape[0], _lib.ptr(surf_in), _lib.stream(o.device))
         return F.relu(self.surf_mlp(self.surf_encoder(surf_in)))
 
+    def _surface_async(self, ray_batch):
+        """Start the surface branch on the side stream; returns a callable giving its
+        output on the current stream. ``surface_stream = False`` (or
+        ANR_SURFACE_STREAM=0) keeps everything on one stream."""
+        dev = ray_batch["origin"].device
+        if not self.surface_stream or dev.type != "cuda":
+            out = self._surface(ray_batch)
+            return lambda: out
+        main = torch.cuda.current_stream(dev)
+        side = _lib.side_stream(dev)
+        side.wait_stream(main)  # batch rows (gathered on main), f16 copies (AdamW on main)
+        with torch.cuda.stream(side):
+            out = self._surface(ray_batch)
+            if out.requires_grad:
+                out = _lib.JoinAtBackwardEnd.apply(out, main)
+
+        def join():
+            main.wait_stream(side)
+            out.record_stream(main)
+            return out
+        return join
+
     def _forward_fused(self, ray_batch, u=None):
         B = ray_batch["origin"].shape[0]
         N = self.config["num_samples_per_ray"]
+        # the per-ray surface branch (6 small kernels each way) is enqueued first, on its
+        # own stream, so it runs beside the sampler / hash grid forward and, in backward,
+        # beside the hash-grid backward
+        surf_branch = self._surface_async(ray_batch)
         _, z_vals, coords = sample_and_preprocess(ray_batch, N, self._prep_ngp, u=u)
         occ = self.occupancy
         if occ is not None and self.training:
@@ -148,7 +176,7 @@ class InstantNGPPipeline(Pipeline):
                                              *params)
         color = color.view(B, N, -1)
         sigma = sigma.view(B, N, 1)
-        color_surf = self._surface(ray_batch)
+        color_surf = surf_branch()
         color_map, _, weights, atmo, surf = render_with_surface(
             z_vals, color, sigma, color_surf, z_scale=self.scale / 1000)
         return {

@@ -128,3 +128,33 @@ def test_bucket_zeroed_by_adam_matches_fill(scene, dev):
     for m in runs[0]:
         a, b = runs[0][m], runs[1][m]
         assert ((a - b).norm() / a.norm()).item() <= 1e-3, m
+
+
+def test_surface_branch_stream_matches_single_stream(scene, dev):
+    """The surface branch runs on a side stream (InstantNGPPipeline._surface_async) and its
+    backward writes the surface gradients straight into a FlatGradBucket; the gradients
+    read on the caller's stream right after backward() must equal a one-stream run's
+    (JoinAtBackwardEnd makes the caller's stream wait). Atomics order only: 1e-5."""
+    from atmonr_amd.batch_loader import BatchLoader
+    from atmonr_amd.parallel import FlatGradBucket
+
+    batch = next(iter(BatchLoader(scene, 4096, seed=3)))
+    u = torch.rand(4096, 64, device=dev)
+    grads, outs = {}, {}
+    for side in (False, True):
+        p = _pipe(scene, dev, fused=True, dtype=torch.float16)
+        p.surface_stream = side
+        FlatGradBucket([q for m in p.modules() for q in m.parameters()], dev)
+        res = p.forward(batch, u=u)
+        p.compute_loss(batch, res).backward()
+        # read on the caller's stream immediately (no synchronize in between)
+        grads[side] = {m: getattr(p, m).params.grad.clone()
+                       for m in ("surf_encoder", "surf_mlp", "pos_encoder", "pos_mlp")}
+        outs[side] = res["color_map_fine"].float().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(outs[False], outs[True])
+    for m, g in grads[False].items():
+        h = grads[True][m]
+        assert g.abs().max() > 0, m
+        assert (g - h).abs().max() <= 1e-5 * g.abs().max(), m
+

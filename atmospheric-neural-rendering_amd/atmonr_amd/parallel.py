@@ -82,6 +82,7 @@ class FlatGradBucket:
             p._anr_bucket = self
         self._pending = {id(p): 0 for p in self.params}
         self._works = [None] * len(self._chunks)
+        self._done_ev = {}  # chunk -> events on the streams its gradients were finished on
         self.early_issued = 0  # chunks issued before all_reduce() in the last step
         self._early = 0
 
@@ -101,6 +102,13 @@ class FlatGradBucket:
             return
         self._pending[id(p)] -= 1
         c = self._chunk_of[id(p)]
+        if self.flat.is_cuda and self._distributed(self._group):
+            # the stream this gradient was finished on (the surface branch runs on a side
+            # stream): the chunk's all-reduce waits for every such stream, not only the
+            # one current when the chunk's last gradient completes
+            ev = torch.cuda.Event()
+            ev.record()
+            self._done_ev.setdefault(c, []).append(ev)
         if self._works[c] is None and all(self._pending[id(self.params[i])] <= 0
                                           for i in self._chunks[c][2]):
             self._issue(c)
@@ -109,6 +117,10 @@ class FlatGradBucket:
     def _issue(self, c) -> None:
         s, e, _ = self._chunks[c]
         if self._distributed(self._group):
+            if self.flat.is_cuda:
+                cur = torch.cuda.current_stream(self.flat.device)
+                for ev in self._done_ev.pop(c, ()):
+                    cur.wait_event(ev)
             self._works[c] = dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.AVG,
                                              group=self._group, async_op=True)
         else:
@@ -127,6 +139,7 @@ class FlatGradBucket:
                     w.wait()
             self.early_issued = self._early
             self._works = [None] * len(self._chunks)
+            self._done_ev = {}
             self._pending = {k: 0 for k in self._pending}
             self._early = 0
             return

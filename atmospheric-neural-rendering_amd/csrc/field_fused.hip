@@ -23,7 +23,9 @@
 // per wavefront (pre-pass over |dL/dcolor| and |dL/dsigma|) and unscaled in f32.
 // dL/dpos_out never leaves the registers; the kernel writes only dL/denc (f32).
 
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "anr_common.h"
 
@@ -943,9 +945,40 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 // ---------------------------------------------------------------------------------
 static int g_target_log2 = 6;  // f16 gradient scale: max |dL/dout| of a wavefront -> 2^6
 
-// scratch for the per-wavefront gradient maxima of the backward (grown on demand)
-static float* g_wmax = nullptr;
-static int64_t g_wmax_n = 0;
+// Scratch for the per-wavefront gradient maxima of the backward (nw floats, ≤ 4 KB on
+// 256 CUs): one buffer per (device, stream), so backward launches on different devices or
+// concurrent streams never share it; grown on demand, kept for the process lifetime.
+struct WmaxScratch {
+  int device;
+  hipStream_t stream;
+  float* ptr;
+  int64_t n;
+};
+static std::mutex g_wmax_mu;
+static std::vector<WmaxScratch> g_wmax;
+
+static float* wmax_scratch(hipStream_t st, int64_t nw) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(g_wmax_mu);
+  for (auto& w : g_wmax) {
+    if (w.device != dev || w.stream != st) continue;
+    if (w.n < nw) {
+      // the previous launch on this stream may still read it: free in stream order
+      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+      (void)hipFree(w.ptr);
+      w.ptr = nullptr;
+      w.n = 0;
+      if (hipMalloc(&w.ptr, nw * sizeof(float)) != hipSuccess) return nullptr;
+      w.n = nw;
+    }
+    return w.ptr;
+  }
+  float* p = nullptr;
+  if (hipMalloc(&p, nw * sizeof(float)) != hipSuccess) return nullptr;
+  g_wmax.push_back({dev, st, p, nw});
+  return p;
+}
 
 template <int W, int NHD>
 static int run(int op, const Args& a, hipStream_t st) {
@@ -987,27 +1020,22 @@ static int run(int op, const Args& a, hipStream_t st) {
   if (blocks < 1) blocks = 1;
   const int64_t nw = blocks * waves;
   const int64_t tpw = (tiles + nw - 1) / nw;
-  if (g_wmax_n < nw) {
-    if (g_wmax) (void)hipFree(g_wmax);
-    g_wmax = nullptr;
-    g_wmax_n = 0;
-    if (hipMalloc(&g_wmax, nw * sizeof(float)) != hipSuccess) return 2;
-    g_wmax_n = nw;
-  }
+  float* wmax = wmax_scratch(st, nw);
+  if (!wmax) return 2;
   const float target = ldexpf(1.0f, g_target_log2);
   const dim3 grid(static_cast<unsigned>(blocks)), block(64 * waves);
   if (a.rows) {
-    hipLaunchKernelGGL(absmax_kernel<true>, dim3(nw), dim3(256), 0, st, a, tpw * 32, g_wmax);
+    hipLaunchKernelGGL(absmax_kernel<true>, dim3(nw), dim3(256), 0, st, a, tpw * 32, wmax);
     if (fast)
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, true>), grid, block, 0, st, a, target, tpw, g_wmax);
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, true>), grid, block, 0, st, a, target, tpw, wmax);
     else
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, true>), grid, block, 0, st, a, target, tpw, g_wmax);
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, true>), grid, block, 0, st, a, target, tpw, wmax);
   } else {
-    hipLaunchKernelGGL(absmax_kernel<false>, dim3(nw), dim3(256), 0, st, a, tpw * 32, g_wmax);
+    hipLaunchKernelGGL(absmax_kernel<false>, dim3(nw), dim3(256), 0, st, a, tpw * 32, wmax);
     if (fast)
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, false>), grid, block, 0, st, a, target, tpw, g_wmax);
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, false>), grid, block, 0, st, a, target, tpw, wmax);
     else
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, false>), grid, block, 0, st, a, target, tpw, g_wmax);
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, false>), grid, block, 0, st, a, target, tpw, wmax);
   }
   return 0;
 }

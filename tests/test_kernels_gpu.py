@@ -179,6 +179,41 @@ def test_hashgrid_fwd_bwd_f32(dev, hash_path, cfg, M, coherent):
     close(dtab, gref, rel=1e-5, atol=1e-5)
 
 
+def test_hashgrid_bench_size_adjoint_and_spot_rows(dev):
+    """Bench size (8192 rays x 1024 samples, the config-3 grid): the chunk lengths chosen
+    only at this size (forward 128, backward 256 samples per chunk) against the oracle on
+    4096 spot rows (forward), and the adjoint identity <g, fwd(t)> = <bwd(g), t> over all
+    8.39 M samples (backward: a missed or doubled corner flush at a chunk end would break
+    it by ~1e-3 of the scale; f32 rounding stays ~1e-7). f32 table and gradients."""
+    from atmonr_amd import _lib
+
+    cfg = (3, 16, 16, 1.3819, 19)
+    B, N = 8192, 1024
+    M = B * N
+    d = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, 19)
+    gen = torch.Generator(device=dev).manual_seed(7)
+    o = torch.rand(B, 1, 3, device=dev, generator=gen)
+    dr = (torch.rand(B, 1, 3, device=dev, generator=gen) - 0.5) * 0.6
+    t = torch.linspace(0, 1, N, device=dev)[None, :, None]
+    x = (o + dr * t).clamp(0, 1).reshape(M, 3).contiguous()
+    table = torch.rand(d.n_params, device=dev, generator=gen) * 2 - 1
+    out = torch.empty(M, 32, device=dev)
+    s = _lib.stream(dev)
+    _lib.call("anr_hashgrid_fwd", ctypes.byref(d), x.data_ptr(), 3, M, table.data_ptr(),
+              _lib.F32, out.data_ptr(), _lib.F32, out.stride(0), s)
+    rows = torch.randint(0, M, (4096,), device=dev, generator=gen)
+    ref = ref_tcnn.hashgrid_fwd(x[rows].cpu().numpy(), table.cpu().numpy(), cfg)
+    close(out[rows], ref, rel=1e-5)
+    g = torch.randn(M, 32, device=dev, generator=gen)
+    dtab = torch.zeros(d.n_params, device=dev)
+    _lib.call("anr_hashgrid_bwd", ctypes.byref(d), x.data_ptr(), 3, M, g.data_ptr(), _lib.F32,
+              g.stride(0), dtab.data_ptr(), s)
+    lhs = torch.dot(g.flatten().double(), out.flatten().double()).item()
+    rhs = torch.dot(dtab.double(), table.double()).item()
+    scale = torch.dot(g.flatten().double().abs(), out.flatten().double().abs()).item()
+    assert abs(lhs - rhs) <= 1e-5 * scale, (lhs, rhs, scale)
+
+
 def test_hashgrid_f16_table_and_strided_output(dev, hash_path):
     from atmonr_amd import _lib
 

@@ -125,6 +125,7 @@ _SIGNATURES = {
     "anr_posenc_width": (c_int32, [POINTER(PosencDesc)]),
     "anr_posenc_fwd": (c_int32, [POINTER(PosencDesc), _P, c_int64, c_int64, _P, c_int64, _P]),
     "anr_posenc_bwd": (c_int32, [POINTER(PosencDesc), _P, c_int64, _P, c_int64, _P, _P]),
+    "anr_relu_bwd_colsum": (c_int32, [_P, _P, c_int64, c_int32, _P, _P, c_int32, _P]),
     "anr_sample_pdf_fwd": (
         c_int32,
         [_P, c_int64, c_int32, _P, _P, _P, _P, c_int64, c_int32, c_int32, _P, _P, _P, _P, _P,

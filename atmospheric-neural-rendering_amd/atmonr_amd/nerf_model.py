@@ -83,10 +83,23 @@ class _LinearReLUFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, weight, y = ctx.saved_tensors
-        g = torch.ops.aten.threshold_backward(g, y, 0)
-        dx = g @ weight if ctx.needs_input_grad[0] else None
-        dw = _weight_grad(g, x) if ctx.needs_input_grad[1] else None
-        db = _column_sum(g) if ctx.needs_input_grad[2] else None
+        g = g.contiguous()
+        M, C = g.shape
+        if C % 4 == 0 and C <= 1024 and y.is_contiguous() and M >= 256:
+            # one pass: mask + per-block column sums (anr_relu_bwd_colsum)
+            from . import _lib
+
+            parts = min(1024, M // 256)
+            gm = torch.empty_like(g)
+            partial = torch.empty(parts, C, device=g.device, dtype=torch.float32)
+            _lib.call("anr_relu_bwd_colsum", _lib.ptr(g), _lib.ptr(y), M, C, _lib.ptr(gm),
+                      _lib.ptr(partial), parts, _lib.stream(g.device))
+            db = partial.sum(0) if ctx.needs_input_grad[2] else None
+        else:
+            gm = torch.ops.aten.threshold_backward(g, y, 0)
+            db = _column_sum(gm) if ctx.needs_input_grad[2] else None
+        dx = gm @ weight if ctx.needs_input_grad[0] else None
+        dw = _weight_grad(gm, x) if ctx.needs_input_grad[1] else None
         return dx, dw, db
 
 

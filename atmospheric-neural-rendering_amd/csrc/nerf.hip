@@ -282,6 +282,55 @@ __global__ void __launch_bounds__(64) sample_pdf_bwd_kernel(PdfArgs a) {
   }
 }
 
+
+// AtmoNeRF Linear+ReLU backward (models/nerf.py:48-93 under autograd): g' = g where the
+// saved output y > 0, else 0 (torch's threshold_backward, exact), and the bias gradient
+// sum_r g'[r, :] as per-block column partial sums in a fixed order (the caller adds the
+// P partial rows), so g' is not read a second time by a separate reduction. Threads:
+// C/4 column quads x (256 / (C/4)) row lanes; block b owns rows [b*R, (b+1)*R).
+__global__ void __launch_bounds__(256) relu_bwd_colsum_kernel(const float* __restrict__ g,
+                                                              const float* __restrict__ y,
+                                                              int64_t M, int C, int64_t R,
+                                                              float* __restrict__ gout,
+                                                              float* __restrict__ partial) {
+  __shared__ float4 red[256];
+  const int nq = C >> 2;
+  const int lanes = blockDim.x / nq;
+  const int q = threadIdx.x % nq, rl = threadIdx.x / nq;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t r1 = r0 + R < M ? r0 + R : M;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (rl < lanes) {
+    for (int64_t r = r0 + rl; r < r1; r += lanes) {
+      const int64_t o = r * C + 4 * q;
+      const float4 gv = *reinterpret_cast<const float4*>(g + o);
+      const float4 yv = *reinterpret_cast<const float4*>(y + o);
+      float4 v;
+      v.x = yv.x > 0.f ? gv.x : 0.f;
+      v.y = yv.y > 0.f ? gv.y : 0.f;
+      v.z = yv.z > 0.f ? gv.z : 0.f;
+      v.w = yv.w > 0.f ? gv.w : 0.f;
+      *reinterpret_cast<float4*>(gout + o) = v;
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (rl == 0) {
+    for (int k = 1; k < lanes; ++k) {
+      const float4 t = red[k * nq + q];
+      acc.x += t.x;
+      acc.y += t.y;
+      acc.z += t.z;
+      acc.w += t.w;
+    }
+    *reinterpret_cast<float4*>(partial + static_cast<int64_t>(blockIdx.x) * C + 4 * q) = acc;
+  }
+}
+
 }  // namespace nerf
 }  // namespace anr
 
@@ -383,5 +432,23 @@ extern "C" int anr_sample_pdf_bwd(const float* weights, int64_t w_ray_stride,
   hipLaunchKernelGGL(sample_pdf_bwd_kernel, dim3(static_cast<unsigned>(B)), dim3(64), 0,
                      reinterpret_cast<hipStream_t>(stream), a);
   ANR_CHECK_LAUNCH("anr_sample_pdf_bwd");
+  return ANR_OK;
+}
+
+extern "C" int anr_relu_bwd_colsum(const float* g, const float* y, int64_t M, int32_t C,
+                                   float* g_out, float* partial, int32_t n_parts,
+                                   anr_stream_t stream) {
+  ANR_CHECK_ARG(M >= 0 && C >= 4 && C <= 1024 && C % 4 == 0 && n_parts >= 1,
+                "anr_relu_bwd_colsum: need M >= 0, C a multiple of 4 in [4, 1024], n_parts >= 1");
+  ANR_CHECK_ARG(partial && (M == 0 || (g && y && g_out)), "anr_relu_bwd_colsum: null pointer");
+  ANR_CHECK_ARG(((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(y) |
+                  reinterpret_cast<uintptr_t>(g_out) | reinterpret_cast<uintptr_t>(partial)) & 15) == 0,
+                "anr_relu_bwd_colsum: pointers must be 16-byte aligned");
+  const int64_t R = M > 0 ? (M + n_parts - 1) / n_parts : 1;
+  // every partial row is written (blocks past the last row write zeros)
+  hipLaunchKernelGGL(anr::nerf::relu_bwd_colsum_kernel, dim3(static_cast<unsigned>(n_parts)),
+                     dim3(256), 0, reinterpret_cast<hipStream_t>(stream), g, y, M, C, R, g_out,
+                     partial);
+  ANR_CHECK_LAUNCH("anr_relu_bwd_colsum");
   return ANR_OK;
 }

@@ -324,6 +324,14 @@ int anr_posenc_fwd(const anr_posenc_desc* d, const float* x, int64_t rows_per_x,
 /* dx (P, n_dims) f32 WRITTEN from dL/dout (P, >= width). */
 int anr_posenc_bwd(const anr_posenc_desc* d, const float* x, int64_t P, const float* dout,
                    int64_t dout_stride, float* dx, anr_stream_t stream);
+/* AtmoNeRF Linear+ReLU backward (models/nerf.py:48-93; replaces autograd's
+ * threshold_backward + bias-gradient reduction): g_out = g where y > 0 else 0, for
+ * contiguous (M, C) f32 g, y, g_out (C a multiple of 4, <= 1024, 16-byte aligned); and
+ * partial (n_parts, C) f32 WRITTEN with the column sums of g_out over n_parts row blocks
+ * (fixed order; the bias gradient is their sum; M = 0 writes zeros, g/y/g_out may be
+ * NULL then). */
+int anr_relu_bwd_colsum(const float* g, const float* y, int64_t M, int32_t C, float* g_out,
+                        float* partial, int32_t n_parts, anr_stream_t stream);
 /* sample_pdf forward, one wavefront per ray (3 <= Nc <= 64, 1 <= Nf <= 256).
  *   weights: coarse render weights, element (b, j) at b*w_ray_stride + j*w_sample_stride
  *   (channel 0 of (B, Nc, S)); z_coarse (B,Nc) f32 ascending; u (B,Nf) f32 draws.

@@ -252,3 +252,25 @@ def test_nerf_training_reduces_loss(scene, dev):
     assert np.mean(losses[-10:]) < 0.8 * np.mean(losses[:10]), losses
     sig = pipe.extract(torch.rand(1000, 3, device=dev) * 2 - 1)
     assert sig.shape == (1000, 4) and bool((sig >= 0).all())
+
+
+@pytest.mark.parametrize("M,C", [(786432, 256), (262144, 128), (5000, 12), (300, 1024), (0, 8)])
+def test_relu_bwd_colsum_matches_torch(dev, M, C):
+    """anr_relu_bwd_colsum (AtmoNeRF Linear+ReLU backward): the masked gradient equals
+    torch's threshold_backward bit for bit; the bias gradient (sum of the per-block
+    partials) equals g'.sum(0) in f64 within f32 summation error (1e-5 of sum |g'|)."""
+    from atmonr_amd import _lib
+
+    gen = torch.Generator(device=dev).manual_seed(M + C)
+    g = torch.randn(M, C, device=dev, generator=gen)
+    y = torch.relu(torch.randn(M, C, device=dev, generator=gen))
+    parts = max(1, min(1024, M // 256))
+    gm = torch.empty_like(g)
+    partial = torch.full((parts, C), float("nan"), device=dev)
+    _lib.call("anr_relu_bwd_colsum", _lib.ptr(g), _lib.ptr(y), M, C, _lib.ptr(gm),
+              _lib.ptr(partial), parts, _lib.stream(dev))
+    ref = torch.ops.aten.threshold_backward(g, y, 0)
+    assert torch.equal(gm, ref)
+    db = partial.sum(0).double()
+    want = ref.double().sum(0)
+    assert torch.all((db - want).abs() <= 1e-5 * ref.double().abs().sum(0) + 1e-30)

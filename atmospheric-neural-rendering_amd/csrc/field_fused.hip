@@ -547,12 +547,29 @@ __device__ __forceinline__ void st4g(_Float16* base, int ld, int mrow, int col, 
 // gradient scale of a wavefront is set from max(|dL/dcolor|, |dL/dsigma|) over its rows,
 // which this kernel computes first (one block per wavefront range, full occupancy).
 template <bool ROWS>
-__global__ void __launch_bounds__(256) absmax_kernel(Args a, int64_t rows_per_wave, float* wmax) {
+__global__ void __launch_bounds__(1024) absmax_kernel(Args a, int64_t rows_per_wave, float* wmax) {
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_wave;
   const int64_t r1 = r0 + rows_per_wave < a.M ? r0 + rows_per_wave : a.M;
   float m = 0.0f;
   if (a.n_out == 4 && (a.d_color_stride & 3) == 0) {
-    for (int64_t rr = r0 + threadIdx.x; rr < r1; rr += blockDim.x) {
+    // four rows per thread per iteration, loads issued before any max (one wait each)
+    const int64_t step = blockDim.x;
+    int64_t rr = r0 + threadIdx.x;
+    for (; rr + 3 * step < r1; rr += 4 * step) {
+      f4 d[4];
+      float sg[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t r = dense_row<ROWS>(a, rr + k * step);
+        d[k] = *reinterpret_cast<const f4*>(a.d_color + r * a.d_color_stride);
+        sg[k] = a.d_sigma ? a.d_sigma[r] : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        m = fmaxf(m, fmaxf(fmaxf(fmaxf(fabsf(d[k][0]), fabsf(d[k][1])),
+                                 fmaxf(fabsf(d[k][2]), fabsf(d[k][3]))), fabsf(sg[k])));
+    }
+    for (; rr < r1; rr += step) {
       const int64_t r = dense_row<ROWS>(a, rr);
       const f4 d = *reinterpret_cast<const f4*>(a.d_color + r * a.d_color_stride);
       m = fmaxf(m, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
@@ -567,7 +584,7 @@ __global__ void __launch_bounds__(256) absmax_kernel(Args a, int64_t rows_per_wa
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  __shared__ float part[4];
+  __shared__ float part[16];
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1025,13 +1042,13 @@ static int run(int op, const Args& a, hipStream_t st) {
   const float target = ldexpf(1.0f, g_target_log2);
   const dim3 grid(static_cast<unsigned>(blocks)), block(64 * waves);
   if (a.rows) {
-    hipLaunchKernelGGL(absmax_kernel<true>, dim3(nw), dim3(256), 0, st, a, tpw * 32, wmax);
+    hipLaunchKernelGGL(absmax_kernel<true>, dim3(nw), dim3(1024), 0, st, a, tpw * 32, wmax);
     if (fast)
       hipLaunchKernelGGL((bwd_kernel<W, NHD, true, true>), grid, block, 0, st, a, target, tpw, wmax);
     else
       hipLaunchKernelGGL((bwd_kernel<W, NHD, false, true>), grid, block, 0, st, a, target, tpw, wmax);
   } else {
-    hipLaunchKernelGGL(absmax_kernel<false>, dim3(nw), dim3(256), 0, st, a, tpw * 32, wmax);
+    hipLaunchKernelGGL(absmax_kernel<false>, dim3(nw), dim3(1024), 0, st, a, tpw * 32, wmax);
     if (fast)
       hipLaunchKernelGGL((bwd_kernel<W, NHD, true, false>), grid, block, 0, st, a, target, tpw, wmax);
     else

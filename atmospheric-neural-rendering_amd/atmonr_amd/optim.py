@@ -43,6 +43,10 @@ class FusedAdam(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
+                if st["step"].device.type != "cpu":
+                    # a checkpoint loaded with map_location=<gpu> puts 'step' on the device;
+                    # keep it on the host so the step count never costs a device sync
+                    st["step"] = st["step"].cpu()
                 st["step"] += 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 # the f16 compute copy of the parameter (_lib.compute_copy), if a module

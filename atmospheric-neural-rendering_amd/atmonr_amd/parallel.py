@@ -81,6 +81,7 @@ class FlatGradBucket:
         for p in self.params:
             p._anr_bucket = self
         self._pending = {id(p): 0 for p in self.params}
+        self._used = set()  # params registered through grad_use this step
         self._works = [None] * len(self._chunks)
         self._done_ev = {}  # chunk -> events on the streams its gradients were finished on
         self.early_issued = 0  # chunks issued before all_reduce() in the last step
@@ -96,6 +97,7 @@ class FlatGradBucket:
     def grad_use(self, p) -> None:
         if self.overlap and id(p) in self._pending:
             self._pending[id(p)] += 1
+            self._used.add(id(p))
 
     def grad_done(self, p) -> None:
         if not self.overlap or id(p) not in self._pending:
@@ -109,8 +111,12 @@ class FlatGradBucket:
             ev = torch.cuda.Event()
             ev.record()
             self._done_ev.setdefault(c, []).append(ev)
-        if self._works[c] is None and all(self._pending[id(self.params[i])] <= 0
-                                          for i in self._chunks[c][2]):
+        # a chunk is ready only when every param in it reported its uses this step and
+        # all of them completed: a param whose gradient autograd accumulates on its own
+        # (never reported) keeps its chunk for all_reduce(), after the whole backward
+        if self._works[c] is None and all(
+                id(self.params[i]) in self._used and self._pending[id(self.params[i])] <= 0
+                for i in self._chunks[c][2]):
             self._issue(c)
             self._early += 1
 
@@ -141,10 +147,23 @@ class FlatGradBucket:
             self._works = [None] * len(self._chunks)
             self._done_ev = {}
             self._pending = {k: 0 for k in self._pending}
+            self._used = set()
             self._early = 0
             return
         if self._distributed(group):
             dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=group)
+
+    def broadcast_params(self, src: int = 0, group=None) -> None:
+        """Make every rank start from rank ``src``'s parameters (replicas whose init draws
+        from an unseeded RNG would otherwise train different weights on one averaged
+        gradient). Cached f16 compute copies are invalidated."""
+        if not self._distributed(group):
+            return
+        with torch.no_grad():
+            for p in self.params:
+                dist.broadcast(p.data, src=src, group=group)
+                if hasattr(p, "_anr_shadow_ver"):
+                    p._anr_shadow_ver = None
 
     @property
     def numel(self) -> int:

@@ -73,8 +73,10 @@ class Trainer:
             raise ValueError(f"batch_size {bs} is not divisible by world size {self.world_size}")
         # all_gpu / num_workers (trainer.py:35-47): the scene is device-resident here, so
         # both settings use the device BatchLoader
+        # the shuffle seed must be the same on every rank (one shared permutation)
         self.dataloader = BatchLoader(dataset, batch_size=bs // self.world_size, shuffle=True,
-                                      rank=self.rank, world_size=self.world_size, seed=seed)
+                                      rank=self.rank, world_size=self.world_size,
+                                      seed=int(config.get("seed", seed)))
         self.epoch_idx = 0
         self.iter_count = 0
         self.num_epochs = int(-(config["num_iters"] // -len(self.dataloader)))
@@ -88,6 +90,10 @@ class Trainer:
             raise NotImplementedError(f"Unknown scheduler type {sch['type']}")
         self.scheduler = ExponentialLR(optimizer=self.optimizer, gamma=gamma)
         self.bucket = FlatGradBucket(pipeline.parameters()) if self.distributed else None
+        if self.bucket is not None:
+            # replicas start from rank 0's weights: modules initialised from the global
+            # torch RNG (nn.Linear in AtmoNeRF) differ per rank otherwise
+            self.bucket.broadcast_params(0)
         now_str = datetime.now().strftime("%Y%m%d_%H%M%S")
         self.log_dir = Path(log_dir) if log_dir is not None else (
             Path("data") / "tensorboard" / f"{exp_name}_{now_str}")
@@ -242,8 +248,11 @@ class Trainer:
         self.log_dir = Path(ckpt["tensorboard_dir"])
         self.epoch_idx = int(ckpt["epoch_idx"])
         self.iter_count = int(ckpt["iter_count"])
+        # continue the shuffle sequence where the checkpointed run left it
+        self.dataloader.epoch = self.epoch_idx
         if self.bucket is not None:  # load_state_dict may have replaced .grad tensors
             self.bucket = FlatGradBucket(self.pipeline.parameters())
+            self.bucket.broadcast_params(0)
 
 
 def lr_at(config: dict, iters_per_epoch: int, iteration: int) -> float:

@@ -115,7 +115,12 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
     from atmonr_amd.pipelines.factory import get_pipeline
 
     torch.manual_seed(0)
-    batch_size = args.batch if args.batch != 8192 else 4096
+    if args.global_batch:
+        if args.global_batch % world:
+            sys.exit(f"--global-batch {args.global_batch} is not divisible by {world} ranks")
+        batch_size = args.global_batch // world
+    else:
+        batch_size = args.batch if args.batch != 8192 else 4096
     pipe = get_pipeline(dict(NERF_CFG), ds)
     pipe.send_tensors_to(dev)
     opt = pipe.get_optimizer({"lr": 5e-4})
@@ -179,7 +184,8 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
         print(json.dumps({
             "metric": "train-step rays/sec", "value": round(value, 1), "unit": "rays/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} "
                     f"HARP2-shaped scene, {len(ds)} rays; random-init weights)",
@@ -193,12 +199,37 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
         dist.destroy_process_group()
 
 
+def _launch_ranks(n: int) -> int:
+    """torch.distributed.run with N local ranks on this script (same arguments), as a
+    child process: rendezvous on 127.0.0.1, one process per GPU."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8192, help="rays per rank per step")
+    ap.add_argument("--batch", type=int, default=8192,
+                    help="rays per rank per step (weak scaling, the default)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: fixed rays per step over all ranks (SURVEY §8(e): "
+                         "8192), each rank takes global/N")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="N > 1 weak-scaling run: skip the extra strong-scaling segment at "
+                         "a global batch of --batch rays")
     ap.add_argument("--samples", type=int, default=1024)
     ap.add_argument("--views", type=int, default=90)
     ap.add_argument("--img-size", type=int, default=512)
@@ -222,6 +253,14 @@ def main():
                     help="untimed steps with every kernel timed (per-kernel breakdown)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            # `bench.py --gpus N` on its own: start N fresh rank processes (this process
+            # has not touched HIP and never will) and exit with their status
+            sys.exit(_launch_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: "
+                 "launch one rank per GPU with --nproc-per-node equal to --gpus")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -249,6 +288,12 @@ def main():
     t_scene = time.time() - t0
     if args.workload == "nerf":
         return run_nerf(args, ds, dev, rank, world, t_scene)
+    if args.global_batch:
+        if args.global_batch % world:
+            sys.exit(f"--global-batch {args.global_batch} is not divisible by {world} ranks")
+        rank_batch, scaling = args.global_batch // world, "strong"
+    else:
+        rank_batch, scaling = args.batch, "weak"
     cfg = ingp_config(args.variant, args.samples)
     dtype = torch.float16 if args.dtype == "f16" else torch.float32
     occ = None
@@ -274,7 +319,7 @@ def main():
         # gradients reduce while the hash-grid backward runs
         bucket.enable_overlap()
 
-    loader = BatchLoader(ds, args.batch, shuffle=True, rank=rank, world_size=world, seed=0)
+    loader = BatchLoader(ds, rank_batch, shuffle=True, rank=rank, world_size=world, seed=0)
     it = iter(loader)
 
     def next_batch():
@@ -305,7 +350,7 @@ def main():
     # Untimed profiling pass: HIP events around every libanr call give the per-kernel
     # breakdown and pick the dominant kernel; the timed region below then brackets only
     # that kernel's launches (events around every call would cost ~0.2 ms per step).
-    M = args.batch * args.samples
+    M = rank_batch * args.samples
     models = kernel_models(pipe, M)
     kernels, dominant = {}, None
     if not args.no_kernel_timer:
@@ -349,8 +394,33 @@ def main():
     final_loss = float(loss.item())
 
     ms_per_step = elapsed / args.steps * 1e3
-    rays_total = args.batch * world * args.steps
+    rays_total = rank_batch * world * args.steps
     value = rays_total / elapsed
+
+    strong = None
+    if world > 1 and scaling == "weak" and not args.no_strong and args.batch % world == 0:
+        # the same job at a fixed global batch of --batch rays (SURVEY §8(e)'s strong-
+        # scaling target), timed the same way after a short warm-up at the new shape
+        loader = BatchLoader(ds, args.batch // world, shuffle=True, rank=rank,
+                             world_size=world, seed=0)
+        it = iter(loader)
+        for _ in range(max(2, args.warmup)):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t1], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+        strong = {"global_batch": args.batch, "per_rank_batch": args.batch // world,
+                  "value": round(args.batch * args.steps / el, 1),
+                  "ms_per_step": round(el / args.steps * 1e3, 3), "steps": args.steps}
 
     roofline = None
     if timer:
@@ -378,7 +448,7 @@ def main():
             if os.path.exists(pmc):
                 try:
                     data = json.load(open(pmc))
-                    key = f"{dominant}:{args.variant}:{args.batch}x{args.samples}"
+                    key = f"{dominant}:{args.variant}:{rank_batch}x{args.samples}"
                     ent = data.get(key)
                     if ent:  # HBM bytes per launch from rocprofv3 PMC (tools/prof.sh)
                         roofline["traffic"] = ent["bytes"]
@@ -404,7 +474,7 @@ def main():
             "ms_per_step": round(ms_per_step, 3),
             "host_ms_per_step": round(t_host / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f16" if dtype == torch.float16 else "f32",
             "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} "
@@ -416,12 +486,14 @@ def main():
                              f"(fwd+loss+bwd+AdamW)"
                              + (" + occupancy-grid culling (BASELINE configs[4], beyond the "
                                 "reference)" if occ is not None else "")),
-                "global_batch": args.batch * world,
+                "global_batch": rank_batch * world,
+                "per_rank_batch": rank_batch,
                 "samples_per_ray": args.samples,
                 "parallelism": f"dp{world}",
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "strong_scaling": strong,
             "kernels": kernels,
             "kernels_source": f"untimed profiling pass of {args.profile_steps} steps",
             "grad_all_reduce": {

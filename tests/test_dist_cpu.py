@@ -173,3 +173,50 @@ def test_overlapped_bucket_matches_plain_all_reduce():
         for k in range(4):
             want = (torch.tensor(out["local0"][step][k]) + torch.tensor(out["local1"][step][k])) / 2
             assert torch.allclose(torch.tensor(g0[step][k]), want, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("n,bs,W", [(1000, 100, 8), (1000, 450, 2), (23587960, 1024, 8),
+                                    (1000, 64, 2), (7, 4, 8), (1024, 128, 8)])
+def test_loader_equal_steps_and_shares(n, bs, W):
+    """Every rank yields len(loader) batches, all ranks' batches of a step have one size,
+    shards are disjoint, and only the rem % W tail rays are dropped (ranks
+    yielding different batch counts mismatch the DP collectives)."""
+    from atmonr_amd.batch_loader import BatchLoader
+
+    loaders = [BatchLoader(_Len(n), bs, rank=r, world_size=W, seed=0)
+               for r in range(W)]
+    sl = [ld.slices() for ld in loaders]
+    L = len(loaders[0])
+    assert all(len(ld) == L and len(s) == L for ld, s in zip(loaders, sl))
+    covered = 0
+    for k in range(L):
+        sizes = {e - s for s, e in (x[k] for x in sl)}
+        assert len(sizes) == 1 and sizes.pop() > 0
+        covered += sum(e - s for s, e in (x[k] for x in sl))
+    starts = sorted(x for s in sl for x in s)
+    assert all(a[1] <= b[0] for a, b in zip(starts, starts[1:]))  # disjoint
+    full = n // (bs * W)
+    rem = n - full * bs * W
+    assert covered == full * bs * W + (rem // W) * W
+
+
+class _Len:
+    device = torch.device("cpu")
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+def test_loader_iterates_tail_shares():
+    from atmonr_amd.batch_loader import BatchLoader
+
+    ds = _Toy(1000)
+    got = [[b["idx"] for b in BatchLoader(ds, 100, rank=r, world_size=8, seed=5)]
+           for r in range(8)]
+    assert [len(g) for g in got] == [2] * 8
+    assert {g[1].numel() for g in got} == {25}
+    allidx = torch.cat([t for g in got for t in g])
+    assert allidx.unique().numel() == 1000

@@ -16,15 +16,16 @@ from tests.conftest import PKG  # noqa: F401  (puts the package on sys.path)
 
 
 class ToyScene:
-    """4 views of 16x16 pixels, every ray valid."""
+    """4 views of 16x16 pixels; the first ``n_valid`` rays are valid (all by default)."""
 
-    def __init__(self, seed=0):
+    def __init__(self, seed=0, n_valid=16 * 16 * 4):
         g = torch.Generator().manual_seed(seed)
         self.device = torch.device("cpu")
         self.img_shp = (16, 16)
         self.view_idx = torch.arange(4)
-        n = 16 * 16 * 4
-        self.ray_filter = torch.ones(n, dtype=torch.bool)
+        self.ray_filter = torch.zeros(16 * 16 * 4, dtype=torch.bool)
+        self.ray_filter[:n_valid] = True
+        n = n_valid
         self.origin = torch.randn(n, 3, generator=g)
         self.ray_irgb_idx = torch.arange(n) % 4
         self.ray_rad = (self.origin.sum(1) + 2).clamp(min=0.1)
@@ -53,8 +54,9 @@ class ToyScene:
 
 class ToyPipeline:
     def __init__(self, seed=0):
-        torch.manual_seed(seed)
-        self.lin = torch.nn.Linear(3, 4)
+        if seed is not None:
+            torch.manual_seed(seed)
+        self.lin = torch.nn.Linear(3, 4)  # seed=None: init from whatever the RNG holds
 
     def parameters(self):
         return self.lin.parameters()
@@ -177,3 +179,58 @@ def test_two_rank_trainer_matches_single_process(tmp_path):
             assert torch.allclose(a, b.detach(), rtol=1e-5, atol=1e-6)
         # progress buffers combined across ranks: every ray recorded on every rank
         assert bool((pix != 0).all())
+
+
+def _dp8_worker(rank, world, port, out):
+    import sys
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from atmonr_amd.trainer import Trainer
+
+    # a different, unseeded init on every rank: the trainer must broadcast rank 0's
+    torch.manual_seed(1000 + rank)
+    pipe = ToyPipeline(seed=None)
+    if rank == 0:
+        out["init"] = [p.detach().clone() for p in pipe.parameters()]
+    # 1000 rays, 100 per rank per step: one full global step (800) + a 200-ray tail
+    # (25 per rank) per epoch; 5 iterations run to the end of the third epoch
+    cfg = _cfg(batch_size=800, num_iters=5, scheduler={"type": "target_lr", "final_lr": 1e-3})
+    tr = Trainer(cfg, ToyScene(n_valid=1000), pipe, log_dir=f"/tmp/anr_dp8_log_{port}_{rank}",
+                 verbose=False)
+    n_batches = [len(list(tr.dataloader)) for _ in range(2)]
+    tr.dataloader.epoch = 0
+    tr.train()
+    out[rank] = ([p.detach().clone() for p in tr.pipeline.parameters()], tr.iter_count,
+                 tr.epoch_idx, n_batches)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_eight_rank_trainer_epoch_tail(tmp_path):
+    """World size 8, n = 1000, 100 rays per rank: every rank yields the same number of
+    equal-size batches (the 200-ray epoch tail splits 25 per rank), Trainer.train runs
+    through three epoch ends without mismatched collectives, the replicas start from rank
+    0's weights although each rank drew its own init, and the result equals one process
+    training on the union batches."""
+    from atmonr_amd.trainer import Trainer
+
+    world = 8
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_dp8_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        params, iters, epochs, n_batches = out[r]
+        assert iters == 5 and epochs == 3 and n_batches == [2, 2]
+    init = out["init"]
+    pipe = ToyPipeline(seed=None)
+    with torch.no_grad():
+        for p, q in zip(pipe.parameters(), init):
+            p.copy_(q)
+    cfg = _cfg(batch_size=800, num_iters=5, scheduler={"type": "target_lr", "final_lr": 1e-3})
+    tr = Trainer(cfg, ToyScene(n_valid=1000), pipe, log_dir=tmp_path, verbose=False)
+    tr.train()
+    for r in range(world):
+        for a, b in zip(out[r][0], tr.pipeline.parameters()):
+            assert torch.allclose(a, b.detach(), rtol=1e-5, atol=1e-6)

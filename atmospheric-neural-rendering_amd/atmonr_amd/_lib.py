@@ -29,7 +29,7 @@ import torch  # noqa: F401  (must precede loading the HIP library)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ANR_HIP_LIB", os.path.join(_HERE, "_native", "libanr_hip.so"))
 
-F32, F16 = 0, 1
+F32, F16, BF16 = 0, 1, 2
 MAX_LEVELS = 32
 
 LOSS_CODES = {
@@ -193,27 +193,29 @@ _SIGNATURES = {
     "anr_ingp_field_supported": (c_int32, [POINTER(MlpDesc), POINTER(MlpDesc)]),
     "anr_ingp_field_packed_size": (c_int64, [POINTER(MlpDesc), POINTER(MlpDesc)]),
     "anr_ingp_field_set_grad_scale": (c_int32, [c_int32]),
+    "anr_ingp_field_bwd_workspace_bytes": (
+        c_int64, [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, c_int64]),
     "anr_ingp_field_pack": (
-        c_int32, [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, _P, _P]),
+        c_int32, [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, _P, _P]),
     "anr_ingp_field_fwd": (
         c_int32,
-        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
-         c_int64, _P],
+        [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64,
+         _P, _P, c_int64, _P],
     ),
     "anr_ingp_field_bwd": (
         c_int32,
-        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
-         c_int64, _P, c_int64, _P, _P, _P],
+        [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64,
+         _P, _P, c_int64, _P, c_int64, _P, _P, _P, c_int64, _P],
     ),
     "anr_ingp_field_fwd_rows": (
         c_int32,
-        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
-         _P, c_int64, _P],
+        [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64,
+         _P, _P, _P, c_int64, _P],
     ),
     "anr_ingp_field_bwd_rows": (
         c_int32,
-        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
-         _P, c_int64, _P, c_int64, _P, _P, _P],
+        [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64,
+         _P, _P, _P, c_int64, _P, c_int64, _P, _P, _P, c_int64, _P],
     ),
     "anr_occupancy_n_blocks": (c_int64, [c_int64]),
     "anr_occupancy_count": (

@@ -21,7 +21,10 @@ gradient for that parameter — the same result as autograd's accumulation, one 
 With f16 networks of the shapes both reference configs use (pos 32->W->16, dir 19->W(x1|2)
 ->nb, W in {32, 64}) the two MLPs and the dir encoding run as ONE kernel each way
 (anr_ingp_field_fwd/bwd): pos_out and dL/dpos_out stay in registers, the backward writes
-only dL/denc. The weights are packed into MFMA fragment order once per forward.
+only dL/denc. The weights are packed into MFMA fragment order once per forward. bf16
+networks (BASELINE configs[4]: f16 hash features, bf16 MFMA MLP) run only this way.
+The backward's workspace (per-wavefront f16 gradient maxima) is allocated here, through
+torch's caching allocator, at anr_ingp_field_bwd_workspace_bytes.
 """
 
 from __future__ import annotations
@@ -70,26 +73,30 @@ class IngpFieldFn(torch.autograd.Function):
         ctx.n_per_ray = n_per_ray
         ctx.params = (p_hash, p_pos, p_dir)
         ctx.rows = rows
-        if rows is not None and not (field_fused(pipe) and enc.dtype == torch.float16):
+        fused = field_fused(pipe) and enc.dtype == torch.float16
+        if rows is not None and not fused:
             raise _lib.ANRError("occupancy culling needs the fused f16 field")
-        if field_fused(pipe) and enc.dtype == torch.float16:
+        if cdt == torch.bfloat16 and not fused:
+            raise _lib.ANRError("bf16 networks run only in the fused field (f16 hash features)")
+        if fused:
+            mma = _mma_code(pipe)
             pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
             packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc),
-                                 device=dev, dtype=torch.float16)
+                                 device=dev, dtype=torch.float16)  # 16-bit carrier
             m_pos, m_dir = p_pos.detach().float(), p_dir.detach().float()  # f32 masters
-            call("anr_ingp_field_pack", pdesc, ddesc, ptr(m_pos), ptr(m_dir), ptr(packed), s,
-                 tag="field_pack")
+            call("anr_ingp_field_pack", pdesc, ddesc, mma, ptr(m_pos), ptr(m_dir), ptr(packed),
+                 s, tag="field_pack")
             nb = pipe.dir_mlp.n_output_dims
             if rows is None:
                 sigma = torch.empty(M, device=dev, dtype=torch.float32)
                 color = torch.empty(M, nb, device=dev, dtype=torch.float32)
-                call("anr_ingp_field_fwd", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
+                call("anr_ingp_field_fwd", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc.stride(0),
                      ptr(dirs), n_per_ray, M, ptr(sigma), ptr(color), color.stride(0), s,
                      tag="field_fwd")
             else:
                 sigma = torch.zeros(m_dense, device=dev, dtype=torch.float32)
                 color = torch.zeros(m_dense, nb, device=dev, dtype=torch.float32)
-                call("anr_ingp_field_fwd_rows", pdesc, ddesc, ptr(packed), ptr(enc),
+                call("anr_ingp_field_fwd_rows", pdesc, ddesc, mma, ptr(packed), ptr(enc),
                      enc.stride(0), ptr(dirs), n_per_ray, M, ptr(rows), ptr(sigma), ptr(color),
                      color.stride(0), s, tag="field_fwd")
             ctx.fused_field = True
@@ -164,15 +171,19 @@ class IngpFieldFn(torch.autograd.Function):
         d_sigma = d_sigma.float().contiguous() if d_sigma is not None else None
         d_enc = torch.empty(M, enc.shape[1], device=dev, dtype=torch.float32)
         pdesc, ddesc = ctypes.byref(pipe.pos_mlp.desc), ctypes.byref(pipe.dir_mlp.desc)
+        mma = _mma_code(pipe)
+        ws_bytes = _lib.load().anr_ingp_field_bwd_workspace_bytes(pdesc, ddesc, mma, M)
+        ws = torch.empty(max(1, -(-ws_bytes // 4)), device=dev, dtype=torch.float32)
         if ctx.rows is None:
-            call("anr_ingp_field_bwd", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
+            call("anr_ingp_field_bwd", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc.stride(0),
                  ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color), d_color.stride(0),
-                 ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), s, tag="field_bwd")
-        else:  # dL/d(sigma, color) are dense; read at the kept samples' rows
-            call("anr_ingp_field_bwd_rows", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
-                 ptr(dirs), ctx.n_per_ray, M, ptr(ctx.rows), ptr(d_sigma), ptr(d_color),
-                 d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), s,
+                 ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), ptr(ws), ws_bytes, s,
                  tag="field_bwd")
+        else:  # dL/d(sigma, color) are dense; read at the kept samples' rows
+            call("anr_ingp_field_bwd_rows", pdesc, ddesc, mma, ptr(packed), ptr(enc),
+                 enc.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(ctx.rows), ptr(d_sigma),
+                 ptr(d_color), d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos),
+                 ptr(g_dir), ptr(ws), ws_bytes, s, tag="field_bwd")
         _done(direct_p, p_pos, direct_d, p_dir)  # MLP grads final: their all-reduce may start
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
@@ -181,14 +192,54 @@ class IngpFieldFn(torch.autograd.Function):
                 None if direct_d else g_dir, None, None, None)
 
 
+def _mma_code(pipe) -> int:
+    return _lib.BF16 if pipe.pos_mlp.dtype == torch.bfloat16 else _lib.F16
+
+
 def field_fused(pipe) -> bool:
     """True when the pipeline's networks run through anr_ingp_field_{fwd,bwd}."""
     flag = getattr(pipe, "_field_fused", None)
     if flag is None:
-        ok = (pipe.pos_mlp.dtype == torch.float16 and pipe.dir_mlp.dtype == torch.float16
+        ok = (pipe.pos_mlp.dtype in (torch.float16, torch.bfloat16)
+              and pipe.dir_mlp.dtype == pipe.pos_mlp.dtype
+              and (pipe.pos_mlp.dtype == torch.float16
+                   or pipe.pos_encoder.dtype == torch.float16)
               and getattr(pipe, "allow_field_fusion", True))
         if ok:
             ok = bool(_lib.load().anr_ingp_field_supported(ctypes.byref(pipe.pos_mlp.desc),
                                                            ctypes.byref(pipe.dir_mlp.desc)))
         pipe._field_fused = flag = ok
     return flag
+
+
+@torch.no_grad()
+def field_density(pipe, pts: torch.Tensor) -> torch.Tensor:
+    """sigma = relu(pos_mlp(pos_encoder(pts))[:, 0]) at hash-grid points (P, 3) through the
+    fused field kernels (hash forward, then anr_ingp_field_fwd, whose sigma output is
+    exactly this; the colour it also computes is discarded). The extract path of
+    instant_ngp.py:208-247 and the occupancy grid's density function, for pipelines whose
+    field is fused (the only path for bf16 networks)."""
+    dev = pts.device
+    s = _lib.stream(dev)
+    P = pts.shape[0]
+    sigma = torch.empty(P, device=dev, dtype=torch.float32)
+    if P == 0:
+        return sigma
+    enc_mod, pos_mod = pipe.pos_encoder, pipe.pos_mlp
+    grid = enc_mod.hash_grids[0]
+    pts = pts.float().contiguous()
+    t_hash = _lib.compute_copy(enc_mod.params, enc_mod.dtype)
+    enc = torch.empty(P, grid.n_out, device=dev, dtype=torch.float16)
+    call("anr_hashgrid_fwd", ctypes.byref(grid.desc), ptr(pts), 3, P, ptr(t_hash),
+         dtype_code(t_hash.dtype), ptr(enc), _lib.F16, enc.stride(0), s, tag="hash_fwd")
+    mma = _mma_code(pipe)
+    pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
+    packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc), device=dev,
+                         dtype=torch.float16)
+    call("anr_ingp_field_pack", pdesc, ddesc, mma, ptr(pos_mod.params.detach().float()),
+         ptr(pipe.dir_mlp.params.detach().float()), ptr(packed), s, tag="field_pack")
+    dirs = torch.full((1, 3), 0.5, device=dev)  # one "ray" for all points: colour unused
+    color = torch.empty(P, pipe.dir_mlp.n_output_dims, device=dev, dtype=torch.float32)
+    call("anr_ingp_field_fwd", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc.stride(0),
+         ptr(dirs), P, P, ptr(sigma), ptr(color), color.stride(0), s, tag="field_fwd")
+    return sigma

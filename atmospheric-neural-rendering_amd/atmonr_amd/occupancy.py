@@ -126,7 +126,11 @@ def pipeline_density(pipe):
     """density_fn for OccupancyGrid.update: relu(pos_mlp(pos_encoder(p))[:, 0]) of an
     Instant-NGP pipeline at hash-grid points (the extract path without preprocessing)."""
 
+    from .field import field_density, field_fused
+
     def fn(pts: torch.Tensor) -> torch.Tensor:
+        if field_fused(pipe) and pipe.pos_encoder.dtype == torch.float16:
+            return field_density(pipe, pts)
         out = pipe.pos_mlp(pipe.pos_encoder(pts))
         return torch.relu(out[:, 0].float())
 

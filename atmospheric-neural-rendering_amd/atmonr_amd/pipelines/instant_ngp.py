@@ -26,7 +26,7 @@ import torch.nn.functional as F
 from torch.optim import Optimizer
 
 from .. import _lib
-from ..field import IngpFieldFn
+from ..field import IngpFieldFn, field_density, field_fused
 from ..graphics_utils import render_with_surface
 from ..losses import LOSSES, indexed_loss
 from ..occupancy import OccupancyGrid, pipeline_density
@@ -41,7 +41,12 @@ class InstantNGPPipeline(Pipeline):
                     "surf_mlp"]
 
     def __init__(self, config: dict, dataset: Any, dtype: torch.dtype = torch.float16,
-                 fused: bool = True, seed: int = 1337, occupancy=None) -> None:
+                 fused: bool = True, seed: int = 1337, occupancy=None,
+                 mlp_dtype: torch.dtype | None = None) -> None:
+        """``dtype``: tcnn compute precision of every module (f16 as the reference, or f32).
+        ``mlp_dtype=torch.bfloat16`` (BASELINE configs[4], beyond the reference): the
+        per-sample pos / dir MLPs run bf16 MFMA over the f16 hash features (fused field
+        only); the per-ray surface network keeps ``dtype``."""
         super().__init__(config, dataset)
         self.num_density_outputs = 1
         if self.config["multi_band_extinction"]:
@@ -52,17 +57,21 @@ class InstantNGPPipeline(Pipeline):
             fused = False
         self.fused = fused
         self.dtype = dtype
+        mlp_dtype = dtype if mlp_dtype is None else mlp_dtype
+        if mlp_dtype == torch.bfloat16 and (dtype != torch.float16 or not fused):
+            raise ValueError("bf16 field MLPs need f16 hash features and the fused path")
+        self.mlp_dtype = mlp_dtype
         self.surface_stream = os.environ.get("ANR_SURFACE_STREAM", "1") != "0"
         ingp = self.config["instant_ngp"]
         nb = self.config["num_bands"]
         fdt = torch.float32 if fused else None  # fused path keeps activations/grads in f32
         self.pos_encoder = Encoding(3, ingp["encoding"], seed=seed, dtype=dtype)
         self.pos_mlp = Network(self.pos_encoder.n_output_dims, 16, ingp["network"],
-                               seed=seed + 1, dtype=dtype)
+                               seed=seed + 1, dtype=mlp_dtype)
         self.dir_encoder = Encoding(3 + 16 - self.num_density_outputs, ingp["dir_encoding"],
                                     seed=seed + 2, dtype=dtype)
         self.dir_mlp = Network(self.dir_encoder.n_output_dims, nb, ingp["rgb_network"],
-                               seed=seed + 3, dtype=dtype)
+                               seed=seed + 3, dtype=mlp_dtype)
         self.surf_encoder = Encoding(2 + 3, ingp["surface_encoding"], seed=seed + 4,
                                      dtype=dtype, output_dtype=fdt)
         self.surf_mlp = Network(self.surf_encoder.n_output_dims, nb, ingp["surface_network"],
@@ -229,6 +238,10 @@ class InstantNGPPipeline(Pipeline):
         else:
             pts = (pts + 1) / 2
             pts[..., 2] = pts[..., 2] / self.alt_compress
+        if self.num_density_outputs == 1 and field_fused(self) and \
+                self.pos_encoder.dtype == torch.float16:
+            # the fused field's sigma output IS relu(pos_out[:, 0])
+            return field_density(self, pts).view(pts.shape[0], 1)
         with torch.no_grad():
             pos_out = self.pos_mlp(self.pos_encoder(pts))
         return torch.clip(pos_out[..., : self.num_density_outputs].view(

@@ -245,7 +245,7 @@ class _NetworkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, params, net: "Network"):
         M = x.shape[0]
-        prec = _lib.F16 if net.dtype == torch.float16 else _lib.F32
+        prec = _net_prec(net)
         p = _lib.compute_copy(params, net.dtype)
         out = torch.empty(M, net.n_output_dims, device=x.device, dtype=net.output_dtype)
         call("anr_mlp_fwd", ctypes.byref(net.desc), prec, ptr(p), ptr(x), dtype_code(x.dtype),
@@ -260,7 +260,7 @@ class _NetworkFn(torch.autograd.Function):
         x, p = ctx.saved_tensors
         net: Network = ctx.net
         dout = dout.contiguous()
-        prec = _lib.F16 if net.dtype == torch.float16 else _lib.F32
+        prec = _net_prec(net)
         dparams, direct = _lib.grad_target(net.params, x.device)
         din = None
         if ctx.needs_input_grad[0]:
@@ -277,6 +277,17 @@ class _NetworkFn(torch.autograd.Function):
         if direct:
             _lib.grad_done(net.params)
         return din, None if direct else dparams, None
+
+
+def _net_prec(net) -> int:
+    """Compute precision code of a standalone network kernel (anr_mlp_*): f16 or f32. bf16
+    networks exist only inside the fused Instant-NGP field (anr_ingp_field_*)."""
+    if net.dtype == torch.float16:
+        return _lib.F16
+    if net.dtype == torch.float32:
+        return _lib.F32
+    raise ANRError(f"Network dtype {net.dtype}: standalone MLP kernels run f16 or f32; bf16 "
+                   "is the fused Instant-NGP field's MFMA precision only")
 
 
 class Network(nn.Module):

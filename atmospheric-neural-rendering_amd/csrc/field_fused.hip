@@ -23,9 +23,7 @@
 // per wavefront (pre-pass over |dL/dcolor| and |dL/dsigma|) and unscaled in f32.
 // dL/dpos_out never leaves the registers; the kernel writes only dL/denc (f32).
 
-#include <mutex>
 #include <type_traits>
-#include <vector>
 
 #include "anr_common.h"
 
@@ -60,27 +58,57 @@ __device__ unsigned long long g_stamp[16];
 #define STAMP(k) do {} while (0)
 #endif
 
+// 16-bit operand carriers. With BF = false they hold f16 values; with BF = true
+// (BASELINE configs[4]: bf16 MFMA MLP over the f16 hash features) the same vectors carry
+// bf16 bit patterns: only the MFMA opcodes, the f32 -> 16-bit conversions, the ReLU and
+// the constants differ, everything in between (LDS tiles, transposed reads, ReLU masks
+// on the bits) is type-blind.
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef short s4v __attribute__((vector_size(8)));
+typedef short s4e __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4v lds_s4v;
 
+template <bool BF>
 __device__ __forceinline__ f4 mma32(h8 a, h8 b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  if constexpr (BF)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a),
+                                                   __builtin_bit_cast(b8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 // dW accumulation: the accumulator lives in AGPRs for the whole kernel (the rest of the
 // kernel's MFMAs write VGPRs). The compiler does not see these as MFMAs, so every VALU
 // access to an accumulator goes through agpr_fence() first (result-latency wait states).
+template <bool BF>
 __device__ __forceinline__ void mma32_acc(f4& acc, h8 a, h8 b) {
   if constexpr ((FIELD_EXP & 1) != 0) return;
-  asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  if constexpr (BF)
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 __device__ __forceinline__ void agpr_fence() {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 }
+template <bool BF>
 __device__ __forceinline__ f4 mma16(h4 a, h4 b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+  if constexpr (BF)
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4e, a),
+                                                     __builtin_bit_cast(s4e, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+}
+// one f32 -> the 16-bit operand type (round to nearest even), as bits in a _Float16
+template <bool BF>
+__device__ __forceinline__ _Float16 cvt1(float v) {
+  if constexpr (BF)
+    return __builtin_bit_cast(_Float16, static_cast<__bf16>(v));
+  else
+    return static_cast<_Float16>(v);
 }
 
 // B-operand slot k' (0..31) of a 32-wide K block -> unit index when the operand is the
@@ -135,7 +163,7 @@ struct Net {
 // ---------------------------------------------------------------------------------
 // weight packing (f32 master params -> f16 fragments)
 // ---------------------------------------------------------------------------------
-template <int W, int NHD>
+template <int W, int NHD, bool BF>
 __global__ void pack_kernel(const float* __restrict__ pp, const float* __restrict__ pd,
                             _Float16* __restrict__ out) {
   using N = Net<W, NHD>;
@@ -192,7 +220,7 @@ __global__ void pack_kernel(const float* __restrict__ pp, const float* __restric
     const int kt = f / N::KB, kb = f - kt * N::KB;
     v = pp[N::P0 + (32 * kb + perm32(k)) * 32 + 16 * kt + r];
   }
-  out[e] = static_cast<_Float16>(v);
+  out[e] = cvt1<BF>(v);
 }
 
 struct Args {
@@ -229,12 +257,36 @@ __device__ __forceinline__ int64_t dense_row(const Args& a, int64_t row) {
 __device__ __forceinline__ h8 cat(h4 a, h4 b) {
   return h8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 }
-// f32 accumulators -> f16 (round to nearest even, v_cvt_pk_f16_f32) -> ReLU (v_pk_max_f16)
-__device__ __forceinline__ h4 relu_h4(f4 v) {
-  const h4 x = __builtin_convertvector(v, h4);
-  return __builtin_elementwise_max(x, h4{0, 0, 0, 0});
+// f32 accumulators -> 16-bit (round to nearest even, v_cvt_pk_{f16,bf16}_f32)
+template <bool BF>
+__device__ __forceinline__ h4 to_h4(f4 v) {
+  if constexpr (BF)
+    return __builtin_bit_cast(h4, __builtin_convertvector(v, b4));
+  else
+    return __builtin_convertvector(v, h4);
 }
-__device__ __forceinline__ h4 to_h4(f4 v) { return __builtin_convertvector(v, h4); }
+// -> ReLU: f16 after the conversion (v_pk_max_f16), bf16 before it (v_max_f32)
+template <bool BF>
+__device__ __forceinline__ h4 relu_h4(f4 v) {
+  if constexpr (BF) {
+    return to_h4<true>(__builtin_elementwise_max(v, f4{0.0f, 0.0f, 0.0f, 0.0f}));
+  } else {
+    const h4 x = __builtin_convertvector(v, h4);
+    return __builtin_elementwise_max(x, h4{0, 0, 0, 0});
+  }
+}
+// the f16 hash features as MFMA operands (bf16: f16 -> f32 -> bf16, round to nearest)
+template <bool BF>
+__device__ __forceinline__ h8 enc_in(h8 e) {
+  if constexpr (BF) {
+    const h4 lo = {e[0], e[1], e[2], e[3]}, hi = {e[4], e[5], e[6], e[7]};
+    const h4 a = to_h4<true>(__builtin_convertvector(lo, f4));
+    const h4 b = to_h4<true>(__builtin_convertvector(hi, f4));
+    return h8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  } else {
+    return e;
+  }
+}
 // ReLU derivative: keep g where the forward activation (>= 0, f16) is nonzero. On the bits:
 // v_pk_min_u16(act, 1) is 0 or 1 per half and v_pk_mul_lo_u16 by it keeps or clears g
 // (two instructions per pair; written as asm because the compiler expands it to selects).
@@ -245,9 +297,10 @@ __device__ __forceinline__ uint32_t mask2(uint32_t g, uint32_t act) {
   asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(g), "v"(m));
   return r;
 }
+template <bool BF>
 __device__ __forceinline__ h4 mask_h4(f4 g, h4 act) {
   typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-  const u2 gb = __builtin_bit_cast(u2, to_h4(g)), ab = __builtin_bit_cast(u2, act);
+  const u2 gb = __builtin_bit_cast(u2, to_h4<BF>(g)), ab = __builtin_bit_cast(u2, act);
   return __builtin_bit_cast(h4, u2{mask2(gb.x, ab.x), mask2(gb.y, ab.y)});
 }
 
@@ -290,18 +343,16 @@ __device__ __forceinline__ void load_rows(const Args& a, int64_t row, int g, boo
 }
 
 // Input row of the dir MLP for the sample in this lane (B-operand slots 8g..8g+7).
+template <bool BF>
 __device__ __forceinline__ h8 dir_input(const Rows& in, bool valid, int g, f4 po) {
   if (!valid) return h8{};
   if (g == 0)
-    return h8{static_cast<_Float16>(1.0f), static_cast<_Float16>(po[1]),
-              static_cast<_Float16>(po[2]), static_cast<_Float16>(po[3]),
-              static_cast<_Float16>(0.28209479177387814f),
-              static_cast<_Float16>(-0.48860251190291987f * in.dy),
-              static_cast<_Float16>(0.48860251190291987f * in.dz),
-              static_cast<_Float16>(-0.48860251190291987f * in.dx)};
-  const _Float16 one = static_cast<_Float16>(1.0f);
-  return h8{static_cast<_Float16>(po[0]), static_cast<_Float16>(po[1]),
-            static_cast<_Float16>(po[2]), static_cast<_Float16>(po[3]), one, one, one, one};
+    return h8{cvt1<BF>(1.0f), cvt1<BF>(po[1]), cvt1<BF>(po[2]), cvt1<BF>(po[3]),
+              cvt1<BF>(0.28209479177387814f), cvt1<BF>(-0.48860251190291987f * in.dy),
+              cvt1<BF>(0.48860251190291987f * in.dz), cvt1<BF>(-0.48860251190291987f * in.dx)};
+  const _Float16 one = cvt1<BF>(1.0f);
+  return h8{cvt1<BF>(po[0]), cvt1<BF>(po[1]), cvt1<BF>(po[2]), cvt1<BF>(po[3]), one, one, one,
+            one};
 }
 
 template <int W, int NHD>
@@ -364,14 +415,14 @@ struct NoSink {
 
 // sink: receives every layer input as soon as it is computed (the backward writes them
 // to LDS there, so they need not stay live in registers)
-template <int W, int NHD, int NM, typename WS, typename SK>
+template <int W, int NHD, int NM, bool BF, typename WS, typename SK>
 __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const bool* valid,
                                              int g, Tile<W, NHD>* t, const SK& sink) {
   using N = Net<W, NHD>;
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int mt = 0; mt < NM; ++mt) {
-    t[mt].xe = in[mt].xe;
+    t[mt].xe = enc_in<BF>(in[mt].xe);
     sink.xe(mt, t[mt].xe);
   }
 #pragma unroll
@@ -379,7 +430,7 @@ __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const
     const h8 w = fw.P0(nt);
 #pragma unroll
     for (int mt = 0; mt < NM; ++mt) {
-      t[mt].hp[nt] = relu_h4(mma32(w, t[mt].xe, z4));
+      t[mt].hp[nt] = relu_h4<BF>(mma32<BF>(w, t[mt].xe, z4));
       sink.hp(mt, nt, t[mt].hp[nt]);
     }
   }
@@ -389,11 +440,11 @@ __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const
   for (int kb = 0; kb < N::KB; ++kb) {
     const h8 w = fw.P1(kb);
 #pragma unroll
-    for (int mt = 0; mt < NM; ++mt) t[mt].po = mma32(w, cat(t[mt].hp[2 * kb], t[mt].hp[2 * kb + 1]), t[mt].po);
+    for (int mt = 0; mt < NM; ++mt) t[mt].po = mma32<BF>(w, cat(t[mt].hp[2 * kb], t[mt].hp[2 * kb + 1]), t[mt].po);
   }
 #pragma unroll
   for (int mt = 0; mt < NM; ++mt) {
-    t[mt].xd = dir_input(in[mt], valid[mt], g, t[mt].po);
+    t[mt].xd = dir_input<BF>(in[mt], valid[mt], g, t[mt].po);
     sink.xd(mt, t[mt].xd);
   }
 #pragma unroll
@@ -401,7 +452,7 @@ __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const
     const h8 w = fw.D0(nt);
 #pragma unroll
     for (int mt = 0; mt < NM; ++mt) {
-      t[mt].hd0[nt] = relu_h4(mma32(w, t[mt].xd, z4));
+      t[mt].hd0[nt] = relu_h4<BF>(mma32<BF>(w, t[mt].xd, z4));
       sink.hd0(mt, nt, t[mt].hd0[nt]);
     }
   }
@@ -416,11 +467,11 @@ __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const
         const h8 w = fw.D1(nt * N::KB + kb);
 #pragma unroll
         for (int mt = 0; mt < NM; ++mt)
-          acc[mt] = mma32(w, cat(t[mt].hd0[2 * kb], t[mt].hd0[2 * kb + 1]), acc[mt]);
+          acc[mt] = mma32<BF>(w, cat(t[mt].hd0[2 * kb], t[mt].hd0[2 * kb + 1]), acc[mt]);
       }
 #pragma unroll
       for (int mt = 0; mt < NM; ++mt) {
-        t[mt].hd1[nt] = relu_h4(acc[mt]);
+        t[mt].hd1[nt] = relu_h4<BF>(acc[mt]);
         sink.hd1(mt, nt, t[mt].hd1[nt]);
       }
     }
@@ -433,7 +484,7 @@ __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const
 #pragma unroll
     for (int mt = 0; mt < NM; ++mt) {
       const h4* last = NHD == 2 ? t[mt].hd1 : t[mt].hd0;
-      t[mt].col = mma32(w, cat(last[2 * kb], last[2 * kb + 1]), t[mt].col);
+      t[mt].col = mma32<BF>(w, cat(last[2 * kb], last[2 * kb + 1]), t[mt].col);
     }
   }
 }
@@ -467,7 +518,7 @@ __device__ __forceinline__ void fwd_raw_to_rows(const FwdRaw& r, Rows& in) {
   in.ds = 0.0f;
 }
 
-template <int W, int NHD, bool ROWS>
+template <int W, int NHD, bool ROWS, bool BF>
 __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   // wave index through readfirstlane: the tile loop then runs on scalar registers
@@ -481,7 +532,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   auto body = [&](const Rows& cur, int64_t row) {
     Tile<W, NHD> t;
     const bool valid = row < a.M;
-    tile_forward<W, NHD, 1>(fw, &cur, &valid, g, &t, NoSink{});
+    tile_forward<W, NHD, 1, BF>(fw, &cur, &valid, g, &t, NoSink{});
     if (row < a.M) {
       const int64_t drow = dense_row<ROWS>(a, row);
       if (g == 0) a.sigma[drow] = fmaxf(t.po[0], 0.0f);
@@ -627,7 +678,7 @@ __device__ __forceinline__ void raw_to_rows(const RawRows& r, int g, Rows& in) {
   in.dc = g == 0 ? r.dc : z4;
 }
 
-template <int W, int NHD, bool FAST, bool ROWS>
+template <int W, int NHD, bool FAST, bool ROWS, bool BF>
 __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t tpw,
                                                   const float* wmax) {
   using N = Net<W, NHD>;
@@ -676,7 +727,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
   // f16 gradient scale 2^e of this wavefront (max over its rows -> target); the dW
   // accumulators are never touched by VALU inside the tile loop (they stay in AGPRs)
   float s = 1.0f, inv_s = 1.0f;
-  {
+  if constexpr (!BF) {  // bf16 has f32's exponent range: no scaling
     const float gm = t_begin < t_end ? wmax[w_id] : 0.0f;
     if (gm > 0.0f) {
       int e = static_cast<int>(floorf(log2f(target / gm)));
@@ -748,14 +799,14 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       FwdWeights<W, NHD> fwl;
       fwl.load(wbt, lane);
       __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
-      tile_forward<W, NHD, 2>(fwl, cur, valid, g, t, Sink{Xpe, Xde, Xph, Xd0, Xd1, li, g});
+      tile_forward<W, NHD, 2, BF>(fwl, cur, valid, g, t, Sink{Xpe, Xde, Xph, Xd0, Xd1, li, g});
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         dens[mt] = t[mt].po[0] > 0.0f;
         f4 gv;  // dL/d(color pre-activation), scaled (cur.dc is zero outside g == 0)
 #pragma unroll
         for (int i = 0; i < 4; ++i) gv[i] = t[mt].col[i] > 0.0f ? cur[mt].dc[i] * s : 0.0f;
-        gc[mt] = to_h4(gv);
+        gc[mt] = to_h4<BF>(gv);
         st4g(Ga, LH, mt * 16 + li, 4 * g, gc[mt]);
       }
     }
@@ -778,12 +829,12 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       }
       __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
-      for (int kt = 0; kt < NT; ++kt) mma32_acc(dD2[kt], ga, xl[kt]);
+      for (int kt = 0; kt < NT; ++kt) mma32_acc<BF>(dD2[kt], ga, xl[kt]);
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          dl[mt][kt] = mask_h4(mma16(wf[kt], gc[mt], z4), mk[mt][kt]);
+          dl[mt][kt] = mask_h4<BF>(mma16<BF>(wf[kt], gc[mt], z4), mk[mt][kt]);
           st4g(Gb, LH, mt * 16 + li, 16 * kt + 4 * g, dl[mt][kt]);
         }
       }
@@ -808,17 +859,17 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int kt = 0; kt < NT; ++kt) mma32_acc(dD1[nt * NT + kt], gb[nt], xb[kt]);
+        for (int kt = 0; kt < NT; ++kt) mma32_acc<BF>(dD1[nt * NT + kt], gb[nt], xb[kt]);
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
         f4 acc[2] = {z4, z4};
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf[kt * KB + kb], cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
+          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf[kt * KB + kb], cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          dh0[mt][kt] = mask_h4(acc[mt], mk[mt][kt]);
+          dh0[mt][kt] = mask_h4<BF>(acc[mt], mk[mt][kt]);
           st4g(Ga, LH, mt * 16 + li, 16 * kt + 4 * g, dh0[mt][kt]);
         }
       }
@@ -843,20 +894,20 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        mma32_acc(dD0[nt * 2], gd[nt], x0);
-        mma32_acc(dD0[nt * 2 + 1], gd[nt], x1);
+        mma32_acc<BF>(dD0[nt * 2], gd[nt], x0);
+        mma32_acc<BF>(dD0[nt * 2 + 1], gd[nt], x1);
       }
       f4 acc[2] = {z4, z4};
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf[kb], cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
+        for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf[kb], cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         // pos_out[:, 0] is the density: its gradient is dL/dsigma through the ReLU
         const float dsv = dens[mt] ? cur[mt].ds * s : 0.0f;
         acc[mt][0] = g == 0 ? dsv : acc[mt][0];
-        dpo[mt] = to_h4(acc[mt]);
+        dpo[mt] = to_h4<BF>(acc[mt]);
         st4g(Gfree, LH, mt * 16 + li, 4 * g, dpo[mt]);
       }
     }
@@ -876,12 +927,12 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       }
       __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
-      for (int kt = 0; kt < NT; ++kt) mma32_acc(dP1[kt], ga, xp[kt]);
+      for (int kt = 0; kt < NT; ++kt) mma32_acc<BF>(dP1[kt], ga, xp[kt]);
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          dhp[mt][kt] = mask_h4(mma16(wf[kt], dpo[mt], z4), mk[mt][kt]);
+          dhp[mt][kt] = mask_h4<BF>(mma16<BF>(wf[kt], dpo[mt], z4), mk[mt][kt]);
           st4g(Gdh0, LH, mt * 16 + li, 16 * kt + 4 * g, dhp[mt][kt]);
         }
       }
@@ -898,8 +949,8 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        mma32_acc(dP0[nt * 2], gp[nt], x0);
-        mma32_acc(dP0[nt * 2 + 1], gp[nt], x1);
+        mma32_acc<BF>(dP0[nt * 2], gp[nt], x0);
+        mma32_acc<BF>(dP0[nt * 2 + 1], gp[nt], x1);
       }
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -907,7 +958,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32(wf[kt * KB + kb], cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
+          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf[kt * KB + kb], cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
           const int64_t row = tile * 32 + mt * 16 + li;
@@ -962,48 +1013,47 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 // ---------------------------------------------------------------------------------
 static int g_target_log2 = 6;  // f16 gradient scale: max |dL/dout| of a wavefront -> 2^6
 
-// Scratch for the per-wavefront gradient maxima of the backward (nw floats, ≤ 4 KB on
-// 256 CUs): one buffer per (device, stream), so backward launches on different devices or
-// concurrent streams never share it; grown on demand, kept for the process lifetime.
-struct WmaxScratch {
-  int device;
-  hipStream_t stream;
-  float* ptr;
-  int64_t n;
+// Backward launch geometry: one resident wavefront per slot (4 per block), each owning a
+// contiguous range of 32-sample tiles. The f16 backward needs one float per wavefront of
+// caller-owned workspace for the gradient maxima; bf16 needs none.
+struct BwdGeom {
+  int64_t blocks, nw, tpw;
 };
-static std::mutex g_wmax_mu;
-static std::vector<WmaxScratch> g_wmax;
-
-static float* wmax_scratch(hipStream_t st, int64_t nw) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(g_wmax_mu);
-  for (auto& w : g_wmax) {
-    if (w.device != dev || w.stream != st) continue;
-    if (w.n < nw) {
-      // the previous launch on this stream may still read it: free in stream order
-      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
-      (void)hipFree(w.ptr);
-      w.ptr = nullptr;
-      w.n = 0;
-      if (hipMalloc(&w.ptr, nw * sizeof(float)) != hipSuccess) return nullptr;
-      w.n = nw;
-    }
-    return w.ptr;
+template <int W, int NHD, bool BF>
+static BwdGeom bwd_geom(int64_t M, bool fast) {
+  const int waves = 4;
+  const void* fn = fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true, false, BF>)
+                        : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false, false, BF>);
+  static int pc[2] = {0, 0};
+  int& p = pc[fast ? 1 : 0];
+  if (p == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
+    p = nb;
   }
-  float* p = nullptr;
-  if (hipMalloc(&p, nw * sizeof(float)) != hipSuccess) return nullptr;
-  g_wmax.push_back({dev, st, p, nw});
-  return p;
+  const int64_t tiles = (M + 31) / 32;
+  int64_t blocks = (tiles + waves - 1) / waves;
+  if (blocks > 256LL * p) blocks = 256LL * p;
+  if (blocks < 1) blocks = 1;
+  const int64_t nw = blocks * waves;
+  return {blocks, nw, (tiles + nw - 1) / nw};
 }
 
-template <int W, int NHD>
-static int run(int op, const Args& a, hipStream_t st) {
+template <int W, int NHD, bool BF>
+static int64_t bwd_workspace(int64_t M) {
+  if (BF || M <= 0) return 0;
+  // the larger of the two kernels' wave counts (fast and general d_color layouts)
+  const int64_t a = bwd_geom<W, NHD, BF>(M, true).nw, b = bwd_geom<W, NHD, BF>(M, false).nw;
+  return static_cast<int64_t>(sizeof(float)) * (a > b ? a : b);
+}
+
+template <int W, int NHD, bool BF>
+static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t st) {
   using N = Net<W, NHD>;
   const int waves = 4;
   if (op == 1) {
     const int64_t tiles = (a.M + 15) / 16;
-    const void* fn = reinterpret_cast<const void*>(&fwd_kernel<W, NHD, false>);
+    const void* fn = reinterpret_cast<const void*>(&fwd_kernel<W, NHD, false, BF>);
     static int pc = 0;
     if (pc == 0) {
       int nb = 0;
@@ -1014,53 +1064,42 @@ static int run(int op, const Args& a, hipStream_t st) {
     if (blocks > 256LL * pc) blocks = 256LL * pc;
     if (blocks < 1) blocks = 1;
     if (a.rows)
-      hipLaunchKernelGGL((fwd_kernel<W, NHD, true>), dim3(blocks), dim3(64 * waves), 0, st, a);
+      hipLaunchKernelGGL((fwd_kernel<W, NHD, true, BF>), dim3(blocks), dim3(64 * waves), 0, st, a);
     else
-      hipLaunchKernelGGL((fwd_kernel<W, NHD, false>), dim3(blocks), dim3(64 * waves), 0, st, a);
+      hipLaunchKernelGGL((fwd_kernel<W, NHD, false, BF>), dim3(blocks), dim3(64 * waves), 0, st, a);
     return 0;
   }
   const bool fast = a.n_out == 4 && (a.d_color_stride & 3) == 0 && a.d_sigma != nullptr;
   const size_t lds = (static_cast<size_t>(N::n_packed) + waves * N::wave_lds) * 2;  // static
   if (lds > 160 * 1024) return 1;
-  const void* fn = fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true, false>)
-                        : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false, false>);
-  static int pc = 0;
-  if (pc == 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
-    pc = nb;
-  }
-  const int64_t tiles = (a.M + 31) / 32;
-  // one resident wavefront per slot, each owning a contiguous range of tiles
-  int64_t blocks = (tiles + waves - 1) / waves;
-  if (blocks > 256LL * pc) blocks = 256LL * pc;
-  if (blocks < 1) blocks = 1;
-  const int64_t nw = blocks * waves;
-  const int64_t tpw = (tiles + nw - 1) / nw;
-  float* wmax = wmax_scratch(st, nw);
-  if (!wmax) return 2;
+  const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast);
+  if (!BF && (ws == nullptr || ws_bytes < static_cast<int64_t>(sizeof(float)) * gm.nw)) return 2;
   const float target = ldexpf(1.0f, g_target_log2);
-  const dim3 grid(static_cast<unsigned>(blocks)), block(64 * waves);
+  const dim3 grid(static_cast<unsigned>(gm.blocks)), block(64 * waves);
   if (a.rows) {
-    hipLaunchKernelGGL(absmax_kernel<true>, dim3(nw), dim3(1024), 0, st, a, tpw * 32, wmax);
+    if (!BF) hipLaunchKernelGGL(absmax_kernel<true>, dim3(gm.nw), dim3(1024), 0, st, a, gm.tpw * 32, ws);
     if (fast)
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, true>), grid, block, 0, st, a, target, tpw, wmax);
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, true, BF>), grid, block, 0, st, a, target, gm.tpw, ws);
     else
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, true>), grid, block, 0, st, a, target, tpw, wmax);
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, true, BF>), grid, block, 0, st, a, target, gm.tpw, ws);
   } else {
-    hipLaunchKernelGGL(absmax_kernel<false>, dim3(nw), dim3(1024), 0, st, a, tpw * 32, wmax);
+    if (!BF) hipLaunchKernelGGL(absmax_kernel<false>, dim3(gm.nw), dim3(1024), 0, st, a, gm.tpw * 32, ws);
     if (fast)
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, false>), grid, block, 0, st, a, target, tpw, wmax);
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, false, BF>), grid, block, 0, st, a, target, gm.tpw, ws);
     else
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, false>), grid, block, 0, st, a, target, tpw, wmax);
+      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, false, BF>), grid, block, 0, st, a, target, gm.tpw, ws);
   }
   return 0;
 }
 
 template <int W, int NHD>
-static void launch_pack(const float* pp, const float* pd, _Float16* out, hipStream_t st) {
+static void launch_pack(const float* pp, const float* pd, _Float16* out, bool bf, hipStream_t st) {
   using N = Net<W, NHD>;
-  hipLaunchKernelGGL((pack_kernel<W, NHD>), dim3((N::n_packed + 255) / 256), dim3(256), 0, st, pp, pd, out);
+  const dim3 grid((N::n_packed + 255) / 256);
+  if (bf)
+    hipLaunchKernelGGL((pack_kernel<W, NHD, true>), grid, dim3(256), 0, st, pp, pd, out);
+  else
+    hipLaunchKernelGGL((pack_kernel<W, NHD, false>), grid, dim3(256), 0, st, pp, pd, out);
 }
 
 // (W, NHD) of a supported pos/dir pair, or 0
@@ -1078,14 +1117,20 @@ static int variant(const anr_mlp_desc* pos, const anr_mlp_desc* dir) {
   return pos->width * 10 + dir->n_hidden_layers;
 }
 
-static int dispatch(int v, int op, const Args& a, hipStream_t st) {
+template <bool BF>
+static int dispatch_t(int v, int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t st) {
   switch (v) {
-    case 321: return run<32, 1>(op, a, st);
-    case 322: return run<32, 2>(op, a, st);
-    case 641: return run<64, 1>(op, a, st);
-    case 642: return run<64, 2>(op, a, st);
+    case 321: return run<32, 1, BF>(op, a, ws, ws_bytes, st);
+    case 322: return run<32, 2, BF>(op, a, ws, ws_bytes, st);
+    case 641: return run<64, 1, BF>(op, a, ws, ws_bytes, st);
+    case 642: return run<64, 2, BF>(op, a, ws, ws_bytes, st);
   }
   return 1;
+}
+static int dispatch(int v, bool bf, int op, const Args& a, float* ws, int64_t ws_bytes,
+                    hipStream_t st) {
+  return bf ? dispatch_t<true>(v, op, a, ws, ws_bytes, st)
+            : dispatch_t<false>(v, op, a, ws, ws_bytes, st);
 }
 
 }  // namespace field
@@ -1107,36 +1152,54 @@ extern "C" int64_t anr_ingp_field_packed_size(const anr_mlp_desc* pos, const anr
   return 0;
 }
 
+extern "C" int64_t anr_ingp_field_bwd_workspace_bytes(const anr_mlp_desc* pos,
+                                                      const anr_mlp_desc* dir,
+                                                      int32_t mma_dtype, int64_t M) {
+  if (mma_dtype == ANR_BF16) return 0;
+  switch (variant(pos, dir)) {
+    case 321: return bwd_workspace<32, 1, false>(M);
+    case 322: return bwd_workspace<32, 2, false>(M);
+    case 641: return bwd_workspace<64, 1, false>(M);
+    case 642: return bwd_workspace<64, 2, false>(M);
+  }
+  return 0;
+}
+
 extern "C" int anr_ingp_field_set_grad_scale(int32_t log2_target) {
   const int prev = g_target_log2;
   g_target_log2 = log2_target;
   return prev;
 }
 
+static bool mma_ok(int32_t t) { return t == ANR_F16 || t == ANR_BF16; }
+
 extern "C" int anr_ingp_field_pack(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                   const float* pos_params, const float* dir_params,
-                                   void* packed, anr_stream_t stream) {
+                                   int32_t mma_dtype, const float* pos_params,
+                                   const float* dir_params, void* packed, anr_stream_t stream) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_pack: unsupported pos/dir MLP pair");
+  ANR_CHECK_ARG(mma_ok(mma_dtype), "anr_ingp_field_pack: mma_dtype must be ANR_F16 or ANR_BF16");
   ANR_CHECK_ARG(pos_params && dir_params && packed, "anr_ingp_field_pack: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   _Float16* out = static_cast<_Float16*>(packed);
+  const bool bf = mma_dtype == ANR_BF16;
   switch (v) {
-    case 321: launch_pack<32, 1>(pos_params, dir_params, out, st); break;
-    case 322: launch_pack<32, 2>(pos_params, dir_params, out, st); break;
-    case 641: launch_pack<64, 1>(pos_params, dir_params, out, st); break;
-    case 642: launch_pack<64, 2>(pos_params, dir_params, out, st); break;
+    case 321: launch_pack<32, 1>(pos_params, dir_params, out, bf, st); break;
+    case 322: launch_pack<32, 2>(pos_params, dir_params, out, bf, st); break;
+    case 641: launch_pack<64, 1>(pos_params, dir_params, out, bf, st); break;
+    case 642: launch_pack<64, 2>(pos_params, dir_params, out, bf, st); break;
   }
   ANR_CHECK_LAUNCH("anr_ingp_field_pack");
   return ANR_OK;
 }
 
-static int field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const void* packed,
-                     const void* enc, int64_t enc_stride, const float* dirs, int64_t n_per_ray,
-                     int64_t M, const int32_t* rows, float* sigma, float* color,
-                     int64_t color_stride, anr_stream_t stream) {
+static int field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,
+                     const void* packed, const void* enc, int64_t enc_stride, const float* dirs,
+                     int64_t n_per_ray, int64_t M, const int32_t* rows, float* sigma,
+                     float* color, int64_t color_stride, anr_stream_t stream) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_fwd: unsupported pos/dir MLP pair");
+  ANR_CHECK_ARG(mma_ok(mma_dtype), "anr_ingp_field_fwd: mma_dtype must be ANR_F16 or ANR_BF16");
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_fwd: bad M");
   if (M == 0) return ANR_OK;
   ANR_CHECK_ARG(packed && enc && dirs && sigma && color, "anr_ingp_field_fwd: null pointer");
@@ -1158,19 +1221,22 @@ static int field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const voi
   a.color = color;
   a.color_stride = color_stride;
   a.rows = rows;
-  ANR_CHECK_ARG(dispatch(v, 1, a, reinterpret_cast<hipStream_t>(stream)) == 0,
+  ANR_CHECK_ARG(dispatch(v, mma_dtype == ANR_BF16, 1, a, nullptr, 0,
+                         reinterpret_cast<hipStream_t>(stream)) == 0,
                 "anr_ingp_field_fwd: no kernel for this shape");
   ANR_CHECK_LAUNCH("anr_ingp_field_fwd");
   return ANR_OK;
 }
 
-static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const void* packed,
-                     const void* enc, int64_t enc_stride, const float* dirs, int64_t n_per_ray,
-                     int64_t M, const int32_t* rows, const float* d_sigma,
+static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,
+                     const void* packed, const void* enc, int64_t enc_stride, const float* dirs,
+                     int64_t n_per_ray, int64_t M, const int32_t* rows, const float* d_sigma,
                      const float* d_color, int64_t d_color_stride, float* d_enc,
-                     int64_t d_enc_stride, float* g_pos, float* g_dir, anr_stream_t stream) {
+                     int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
+                     int64_t workspace_bytes, anr_stream_t stream) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_bwd: unsupported pos/dir MLP pair");
+  ANR_CHECK_ARG(mma_ok(mma_dtype), "anr_ingp_field_bwd: mma_dtype must be ANR_F16 or ANR_BF16");
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_bwd: bad M");
   if (M == 0) return ANR_OK;
   ANR_CHECK_ARG(packed && enc && dirs && d_color && d_enc && g_pos && g_dir,
@@ -1199,51 +1265,60 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const voi
   a.g_pos = g_pos;
   a.g_dir = g_dir;
   a.rows = rows;
-  const int rc = dispatch(v, 2, a, reinterpret_cast<hipStream_t>(stream));
-  ANR_CHECK_ARG(rc != 2, "anr_ingp_field_bwd: scratch allocation failed");
+  const int rc = dispatch(v, mma_dtype == ANR_BF16, 2, a, static_cast<float*>(workspace),
+                          workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+  ANR_CHECK_ARG(rc != 2,
+                "anr_ingp_field_bwd: workspace missing or smaller than "
+                "anr_ingp_field_bwd_workspace_bytes()");
   ANR_CHECK_ARG(rc == 0, "anr_ingp_field_bwd: no kernel for this shape");
   ANR_CHECK_LAUNCH("anr_ingp_field_bwd");
   return ANR_OK;
 }
 
 extern "C" int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                  const void* packed, const void* enc, int64_t enc_stride,
-                                  const float* dirs, int64_t n_per_ray, int64_t M, float* sigma,
-                                  float* color, int64_t color_stride, anr_stream_t stream) {
-  return field_fwd(pos, dir, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr, sigma, color,
-                   color_stride, stream);
+                                  int32_t mma_dtype, const void* packed, const void* enc,
+                                  int64_t enc_stride, const float* dirs, int64_t n_per_ray,
+                                  int64_t M, float* sigma, float* color, int64_t color_stride,
+                                  anr_stream_t stream) {
+  return field_fwd(pos, dir, mma_dtype, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
+                   sigma, color, color_stride, stream);
 }
 
 extern "C" int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                  const void* packed, const void* enc, int64_t enc_stride,
-                                  const float* dirs, int64_t n_per_ray, int64_t M,
-                                  const float* d_sigma, const float* d_color,
+                                  int32_t mma_dtype, const void* packed, const void* enc,
+                                  int64_t enc_stride, const float* dirs, int64_t n_per_ray,
+                                  int64_t M, const float* d_sigma, const float* d_color,
                                   int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
-                                  float* g_pos, float* g_dir, anr_stream_t stream) {
-  return field_bwd(pos, dir, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr, d_sigma,
-                   d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, stream);
+                                  float* g_pos, float* g_dir, void* workspace,
+                                  int64_t workspace_bytes, anr_stream_t stream) {
+  return field_bwd(pos, dir, mma_dtype, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
+                   d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir,
+                   workspace, workspace_bytes, stream);
 }
 
 extern "C" int anr_ingp_field_fwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                       const void* packed, const void* enc, int64_t enc_stride,
-                                       const float* dirs, int64_t n_per_ray, int64_t M,
-                                       const int32_t* rows, float* sigma, float* color,
-                                       int64_t color_stride, anr_stream_t stream) {
+                                       int32_t mma_dtype, const void* packed, const void* enc,
+                                       int64_t enc_stride, const float* dirs, int64_t n_per_ray,
+                                       int64_t M, const int32_t* rows, float* sigma,
+                                       float* color, int64_t color_stride,
+                                       anr_stream_t stream) {
   ANR_CHECK_ARG(rows || M == 0, "anr_ingp_field_fwd_rows: null rows");
-  return field_fwd(pos, dir, packed, enc, enc_stride, dirs, n_per_ray, M, rows, sigma, color,
-                   color_stride, stream);
+  return field_fwd(pos, dir, mma_dtype, packed, enc, enc_stride, dirs, n_per_ray, M, rows,
+                   sigma, color, color_stride, stream);
 }
 
 extern "C" int anr_ingp_field_bwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                       const void* packed, const void* enc, int64_t enc_stride,
-                                       const float* dirs, int64_t n_per_ray, int64_t M,
-                                       const int32_t* rows, const float* d_sigma,
+                                       int32_t mma_dtype, const void* packed, const void* enc,
+                                       int64_t enc_stride, const float* dirs, int64_t n_per_ray,
+                                       int64_t M, const int32_t* rows, const float* d_sigma,
                                        const float* d_color, int64_t d_color_stride,
                                        float* d_enc, int64_t d_enc_stride, float* g_pos,
-                                       float* g_dir, anr_stream_t stream) {
+                                       float* g_dir, void* workspace, int64_t workspace_bytes,
+                                       anr_stream_t stream) {
   ANR_CHECK_ARG(rows || M == 0, "anr_ingp_field_bwd_rows: null rows");
-  return field_bwd(pos, dir, packed, enc, enc_stride, dirs, n_per_ray, M, rows, d_sigma,
-                   d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, stream);
+  return field_bwd(pos, dir, mma_dtype, packed, enc, enc_stride, dirs, n_per_ray, M, rows,
+                   d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir,
+                   workspace, workspace_bytes, stream);
 }
 
 #ifdef FIELD_STAMP

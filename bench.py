@@ -32,20 +32,35 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-MFMA_F16_PEAK_TF = 2500.0  # dense fp16/bf16 MFMA (spec, no sparsity)
-MFMA_F32_PEAK_TF = 157.3   # f32-input MFMA (spec)
+# spec-sheet figures (MI355X_MICROARCH.md), used only with --spec-peaks; by default the
+# peaks are MEASURED on the box in the untimed phase (tools/ubench: float4 copy, bare
+# 16x16x32 MFMA loops on random operands, f32 atomic wave-instructions of the hash-grid
+# backward's 16-B segment shape)
+SPEC_PEAKS = {"hbm_copy_gbs": 8000.0, "mfma_f16_tfs": 2500.0, "mfma_bf16_tfs": 2500.0,
+              "mfma_f32_tfs": 157.3, "atomic_seg16_greq_s": 20.3, "source": "spec"}
 
 
-def kernel_models(pipe, M: int) -> dict:
+def measured_peaks(dev, spec: bool) -> dict:
+    if spec:
+        return dict(SPEC_PEAKS)
+    from tools.ubench import peaks as ub
+
+    p = ub.measure(dev)
+    p["source"] = "measured (tools/ubench/peaks.py, this box, this run)"
+    return p
+
+
+def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "") -> dict:
     """Algorithmic work per launch of each hot kernel.
 
-    bytes = SURVEY §8(d)'s per-sample figures (the roofline definition BASELINE.md quotes):
-    hash forward 12 B coordinates + 16 levels x 8 corners x 2 features x 2 B gathered + 64 B
-    written = 588 B; hash backward 64 B dL/dy + 12 B + 2 x 512 B gradient read-modify-write
-    = 1,100 B (no cache reuse counted, so L2/MALL hits can lift it towards or past the HBM
-    peak). compulsory_bytes = every stream read or written once and every table /
-    gradient array once per launch (the floor). flops = dense MFMA work at padded widths.
+    ``bytes`` = compulsory HBM traffic (every per-sample stream read or written once, the
+    table / gradient array once per launch); ``flops`` = dense MFMA work at padded widths.
+    ``survey_bytes`` = SURVEY §8(d)'s per-sample hash figures (forward 12 + 16x8x2x2 + 64 =
+    588 B, backward 64 + 12 + 2 x 512 = 1,100 B), which count every corner access as HBM
+    traffic; L2/MALL serve most of them, so that model reaches the HBM peak without
+    discriminating and is reported beside the bound, not used for it. ``atomic_requests``
+    (hash backward) = memory-side f32 atomic requests per launch from rocprofv3 PMC
+    (profiles/pmc_traffic.json), priced against the measured request ceiling.
     """
     grid = pipe.pos_encoder.hash_grids[0]
     n_table = grid.desc.n_params                # f16 table entries x features
@@ -58,24 +73,41 @@ def kernel_models(pipe, M: int) -> dict:
     f_fwd = mlp_flops(pos) + mlp_flops(dirm)
     nb = dirm.n_output
     enc_b = 2 * grid.n_out                      # f16 features
-    return {
-        "hash_fwd": {"bytes": M * (12 + grid.n_levels * 8 * 2 * 2 + enc_b), "flops": 0.0,
-                     "compulsory_bytes": M * (12 + enc_b) + 2 * n_table},
-        "hash_bwd": {"bytes": M * (64 + 12 + 2 * grid.n_levels * 8 * 2 * 2), "flops": 0.0,
-                     "compulsory_bytes": M * (12 + 4 * grid.n_out) + 8 * n_table},
+    out = {
+        "hash_fwd": {"bytes": M * (12 + enc_b) + 2 * n_table, "flops": 0.0,
+                     "survey_bytes": M * (12 + grid.n_levels * 8 * 2 * 2 + enc_b)},
+        "hash_bwd": {"bytes": M * (12 + 4 * grid.n_out) + 8 * n_table, "flops": 0.0,
+                     "survey_bytes": M * (64 + 12 + 2 * grid.n_levels * 8 * 2 * 2)},
         # enc in, sigma + color out
         "field_fwd": {"bytes": M * (enc_b + 4 + 4 * nb), "flops": M * f_fwd},
         # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; forward recompute + dX + dW
         "field_bwd": {"bytes": M * (enc_b + 4 * nb + 4 + 4 * grid.n_out), "flops": 3 * M * f_fwd},
     }
+    ent = (pmc or {}).get(f"hash_bwd:{key_sfx}")
+    if ent and ent.get("atomic_requests"):
+        out["hash_bwd"]["atomic_requests"] = float(ent["atomic_requests"])
+    return out
 
-def _roof(mdl: dict, avg_ms: float) -> dict:
+
+def _roof(mdl: dict, avg_ms: float, peaks: dict, mfma_key: str) -> dict:
     sec = avg_ms * 1e-3
     gbs = mdl["bytes"] / sec / 1e9
     tfs = mdl["flops"] / sec / 1e12
-    fb, ff = gbs / HBM_PEAK_GBS, tfs / MFMA_F16_PEAK_TF
-    return {"hbm_gbs": round(gbs, 1), "hbm_frac": round(fb, 4), "mfma_tfs": round(tfs, 2),
-            "mfma_frac": round(ff, 4), "bound": "hbm" if fb >= ff else "mfma"}
+    fb, ff = gbs / peaks["hbm_copy_gbs"], tfs / peaks[mfma_key]
+    r = {"hbm_gbs": round(gbs, 1), "hbm_frac": round(fb, 4), "mfma_tfs": round(tfs, 2),
+         "mfma_frac": round(ff, 4), "bound": "hbm" if fb >= ff else "mfma"}
+    if "survey_bytes" in mdl:
+        sg = mdl["survey_bytes"] / sec / 1e9
+        r["survey_model_gbs"] = round(sg, 1)
+        r["survey_model_frac"] = round(sg / peaks["hbm_copy_gbs"], 4)
+    if "atomic_requests" in mdl:
+        rq = mdl["atomic_requests"] / sec / 1e9
+        fa = rq / peaks["atomic_seg16_greq_s"]
+        r["atomic_greq_s"] = round(rq, 3)
+        r["atomic_frac"] = round(fa, 4)
+        if fa >= max(fb, ff):
+            r["bound"] = "atomic"
+    return r
 
 
 def ingp_config(variant: str, n_samples: int) -> dict:
@@ -104,6 +136,7 @@ def nerf_mlp_flops(net, n_rows: int) -> float:
 
 
 def run_nerf(args, ds, dev, rank, world, t_scene):
+    peaks = measured_peaks(dev, args.spec_peaks)
     """configs/nerf.json train step (nerf.py:179-240 + Adam, trainer.py:99-105): coarse
     64 stratified + fine 64+128 pdf samples per ray, two 8x256 AtmoNeRF MLPs (f32 library
     GEMMs), f32 composite, Adam. Batch 4096 rays per rank (nerf.json trainer.batch_size).
@@ -171,8 +204,8 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
                    + nerf_mlp_flops(pipe.nerf["fine"], batch_size * (nc + nf)))
     tfs = flops / (ms * 1e-3) / 1e12
     roofline = {"kernel": "nerf_mlp_gemms (library f32 GEMMs, whole-step time)",
-                "bound": "mfma", "achieved": round(tfs, 2), "peak": MFMA_F32_PEAK_TF,
-                "unit": "TFLOP/s", "frac": round(tfs / MFMA_F32_PEAK_TF, 4), "traffic": None,
+                "bound": "mfma", "achieved": round(tfs, 2), "peak": peaks["mfma_f32_tfs"],
+                "unit": "TFLOP/s", "frac": round(tfs / peaks["mfma_f32_tfs"], 4), "traffic": None,
                 "algorithmic_flops": flops, "units_per_launch": batch_size,
                 "flops_per_unit": flops / batch_size}
     cpu = None
@@ -193,7 +226,8 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
                                    "positional enc + 8x256 MLP, 64 coarse + 192 fine "
                                    "samples/ray), full train step (fwd+loss+bwd+Adam)",
                        "global_batch": batch_size * world, "parallelism": f"dp{world}"},
-            "roofline": roofline, "cpu_baseline": cpu, "final_loss": round(final_loss, 6),
+            "roofline": roofline, "cpu_baseline": cpu, "peaks": peaks,
+            "final_loss": round(final_loss, 6),
             "scene_build_s": round(t_scene, 2)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -221,7 +255,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps first (the bench network's first AdamW steps kill its "
+                         "densities; it is alive again from step ~7: tools/liveness.py)")
     ap.add_argument("--batch", type=int, default=8192,
                     help="rays per rank per step (weak scaling, the default)")
     ap.add_argument("--global-batch", type=int, default=0,
@@ -236,8 +272,12 @@ def main():
     ap.add_argument("--workload", choices=["ingp", "nerf"], default="ingp",
                     help="ingp: BASELINE configs[2] (the headline line); nerf: configs[1]")
     ap.add_argument("--variant", choices=["baseline", "committed"], default="baseline")
-    ap.add_argument("--dtype", choices=["f16", "f32"], default="f16")
+    ap.add_argument("--dtype", choices=["f16", "bf16", "f32"], default="f16",
+                    help="f16: tcnn precision (the reference's); bf16: BASELINE configs[4], "
+                         "f16 hash features + bf16 MFMA field MLP; f32: exact-f32 kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--spec-peaks", action="store_true",
+                    help="price the rooflines against spec-sheet peaks instead of measuring")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--occupancy", action="store_true",
@@ -295,14 +335,16 @@ def main():
     else:
         rank_batch, scaling = args.batch, "weak"
     cfg = ingp_config(args.variant, args.samples)
-    dtype = torch.float16 if args.dtype == "f16" else torch.float32
+    dtype = torch.float32 if args.dtype == "f32" else torch.float16
+    mlp_dtype = torch.bfloat16 if args.dtype == "bf16" else dtype
     occ = None
     if args.occupancy:
         from atmonr_amd.occupancy import OccupancyGrid
 
         occ = OccupancyGrid((128, 128, 32), alt_compress=float(cfg["alt_compress_factor"]),
                             warmup=args.occ_warmup, update_every=16, device=dev)
-    pipe = InstantNGPPipeline(cfg, ds, dtype=dtype, fused=True, seed=1337, occupancy=occ)
+    pipe = InstantNGPPipeline(cfg, ds, dtype=dtype, fused=True, seed=1337, occupancy=occ,
+                              mlp_dtype=mlp_dtype)
     pipe.send_tensors_to(dev)
     opt_cfg = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
     opt = pipe.get_optimizer(opt_cfg)
@@ -351,7 +393,17 @@ def main():
     # breakdown and pick the dominant kernel; the timed region below then brackets only
     # that kernel's launches (events around every call would cost ~0.2 ms per step).
     M = rank_batch * args.samples
-    models = kernel_models(pipe, M)
+    peaks = measured_peaks(dev, args.spec_peaks)
+    mfma_key = {"f32": "mfma_f32_tfs", "bf16": "mfma_bf16_tfs"}.get(args.dtype, "mfma_f16_tfs")
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+        except (OSError, ValueError):
+            pmc = {}
+    pmc_sfx = f"{args.variant}:{rank_batch}x{args.samples}"
+    models = kernel_models(pipe, M, pmc, pmc_sfx)
     kernels, dominant = {}, None
     if not args.no_kernel_timer:
         prof = _lib.KernelTimer()
@@ -364,7 +416,7 @@ def main():
                      "ms_per_step": round(st["total_ms"] / args.profile_steps, 4)}
             mdl = models.get(name)
             if mdl:
-                entry.update(_roof(mdl, st["avg_ms"]))
+                entry.update(_roof(mdl, st["avg_ms"], peaks, mfma_key))
             kernels[name] = entry
         dominant = next((n for n in kernels if "bound" in kernels[n]), None)
     torch.cuda.synchronize()
@@ -427,33 +479,44 @@ def main():
         st = timer.summary().get(dominant)
         if st:  # the dominant kernel, timed live over the timed region
             mdl = models[dominant]
-            k = _roof(mdl, st["avg_ms"])
-            hbm = k["bound"] == "hbm"
-            roofline = {"kernel": dominant, "bound": k["bound"],
-                        "achieved": k["hbm_gbs"] if hbm else k["mfma_tfs"],
-                        "peak": HBM_PEAK_GBS if hbm else MFMA_F16_PEAK_TF,
-                        "unit": "GB/s" if hbm else "TFLOP/s",
-                        "frac": k["hbm_frac"] if hbm else k["mfma_frac"],
+            k = _roof(mdl, st["avg_ms"], peaks, mfma_key)
+            bound = k["bound"]
+            if bound == "atomic":
+                # memory-side f32 atomic requests (16-B segments: the kernel's shape) per
+                # launch, against the measured request ceiling of that shape; in GB/s of
+                # the requests' segment bytes so the unit stays a bandwidth
+                ach, peak, frac = (round(k["atomic_greq_s"] * 16, 1),
+                                   round(peaks["atomic_seg16_greq_s"] * 16, 1), k["atomic_frac"])
+                unit = "GB/s"
+            elif bound == "hbm":
+                ach, peak, frac, unit = k["hbm_gbs"], peaks["hbm_copy_gbs"], k["hbm_frac"], "GB/s"
+            else:
+                ach, peak, frac, unit = k["mfma_tfs"], peaks[mfma_key], k["mfma_frac"], "TFLOP/s"
+            roofline = {"kernel": dominant, "bound": "hbm" if bound == "atomic" else bound,
+                        "ceiling": ("memory-side f32 atomic requests (MI355X_MICROARCH.md "
+                                    "'Global float atomics'), measured at 16-B segments"
+                                    if bound == "atomic" else
+                                    "HBM float4 copy, measured" if bound == "hbm" else
+                                    "dense MFMA loop on random operands, measured"),
+                        "achieved": ach, "peak": peak, "unit": unit, "frac": frac,
                         "traffic": None, "avg_ms": round(st["avg_ms"], 4),
                         "launches": st["launches"], "units_per_launch": M,
-                        "algorithmic_bytes": mdl["bytes"], "algorithmic_flops": mdl["flops"]}
-            roofline["bytes_per_unit"] = mdl["bytes"] / M
-            if "compulsory_bytes" in mdl:
-                # the floor: each stream and the table / gradient array once per launch
-                cb = mdl["compulsory_bytes"]
-                roofline["compulsory_model"] = {
-                    "bytes": cb, "achieved": round(cb / (st["avg_ms"] * 1e-3) / 1e9, 1),
-                    "frac": round(cb / (st["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                try:
-                    data = json.load(open(pmc))
-                    key = f"{dominant}:{args.variant}:{rank_batch}x{args.samples}"
-                    ent = data.get(key)
-                    if ent:  # HBM bytes per launch from rocprofv3 PMC (tools/prof.sh)
-                        roofline["traffic"] = ent["bytes"]
-                except (OSError, ValueError):
-                    pass
+                        "algorithmic_bytes": mdl["bytes"], "algorithmic_flops": mdl["flops"],
+                        "bytes_per_unit": mdl["bytes"] / M,
+                        "fractions": {x: k[x] for x in ("hbm_frac", "mfma_frac", "atomic_frac",
+                                                        "survey_model_frac") if x in k}}
+            if "atomic_requests" in mdl:
+                roofline["atomic_requests_per_launch"] = mdl["atomic_requests"]
+            if "survey_bytes" in mdl:
+                # SURVEY §8(d)'s per-sample model (every corner access as HBM bytes)
+                roofline["survey_model"] = {
+                    "bytes_per_unit": mdl["survey_bytes"] / M,
+                    "achieved": k["survey_model_gbs"], "frac": k["survey_model_frac"]}
+            ent = pmc.get(f"{dominant}:{pmc_sfx}")
+            if ent:  # HBM bytes per launch from rocprofv3 PMC (tools/prof.sh)
+                roofline["traffic"] = ent["bytes"]
+                roofline["traffic_frac_of_measured_hbm"] = round(
+                    ent["bytes"] / (st["avg_ms"] * 1e-3) / 1e9 / peaks["hbm_copy_gbs"], 4)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -476,7 +539,7 @@ def main():
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "f16" if dtype == torch.float16 else "f32",
+            "dtype": args.dtype,
             "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} "
                     f"HARP2-shaped scene, {len(ds)} rays; random-init weights)",
             "config": {
@@ -485,7 +548,10 @@ def main():
                              f"MLP, {args.samples} samples/ray, full train step "
                              f"(fwd+loss+bwd+AdamW)"
                              + (" + occupancy-grid culling (BASELINE configs[4], beyond the "
-                                "reference)" if occ is not None else "")),
+                                "reference)" if occ is not None else "")
+                             + (", f16 hash features + bf16 MFMA field MLP (BASELINE "
+                                "configs[4], beyond the reference)" if args.dtype == "bf16"
+                                else "")),
                 "global_batch": rank_batch * world,
                 "per_rank_batch": rank_batch,
                 "samples_per_ray": args.samples,
@@ -494,6 +560,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "strong_scaling": strong,
+            "peaks": peaks,
             "kernels": kernels,
             "kernels_source": f"untimed profiling pass of {args.profile_steps} steps",
             "grad_all_reduce": {

@@ -18,7 +18,7 @@
  *   - return 0 on success, a negative ANR_E* code on error; anr_last_error() returns a
  *     thread-local message for the last failure. Errors never throw across the ABI;
  *   - sizes are int64; row strides are in ELEMENTS of the tensor's dtype;
- *   - dtype codes: ANR_F32 = 0, ANR_F16 = 1.
+ *   - dtype codes: ANR_F32 = 0, ANR_F16 = 1, ANR_BF16 = 2 (bf16: field MFMA operands only).
  */
 #ifndef ANR_H_
 #define ANR_H_
@@ -29,9 +29,9 @@
 extern "C" {
 #endif
 
-#define ANR_ABI_VERSION 1
+#define ANR_ABI_VERSION 2
 
-enum anr_dtype { ANR_F32 = 0, ANR_F16 = 1 };
+enum anr_dtype { ANR_F32 = 0, ANR_F16 = 1, ANR_BF16 = 2 };
 
 enum anr_status {
   ANR_OK = 0,
@@ -245,31 +245,41 @@ int anr_ingp_dir_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void* p
  * way (replaces pos_mlp -> dir_encoder -> dir_mlp -> relu at instant_ngp.py:163-184).
  * ------------------------------------------------------------------------------------
  * Supported pairs: pos 32 -> W -> 16 (1 hidden layer, no output activation), dir 19 -> W
- * (1 or 2 hidden layers) -> n_output <= 16, W in {32, 64}; f16 compute only.
+ * (1 or 2 hidden layers) -> n_output <= 16, W in {32, 64}.
+ * mma_dtype: ANR_F16 (the reference's tcnn precision: f16 operands, f32 accumulation) or
+ * ANR_BF16 (BASELINE configs[4], beyond the reference: bf16 operands over the same f16
+ * hash features, f32 accumulation; no gradient scaling). Pack, forward and backward of one
+ * network must use the same mma_dtype.
  * Weights: anr_ingp_field_pack converts the f32 master parameters of both networks
- * (tcnn layout) into one f16 buffer of anr_ingp_field_packed_size halves (MFMA fragment
- * order); run it after every optimizer step.
+ * (tcnn layout) into one 16-bit buffer of anr_ingp_field_packed_size elements (MFMA
+ * fragment order); run it after every optimizer step.
  * Forward: enc (M, >=32) f16 (16-byte aligned rows), dirs (M/n_per_ray, 3) f32 ->
  *   sigma (M,) f32 = relu(pos_out[:,0]), color (M, n_output) f32 = relu(dir_mlp(...)).
  * Backward: d_sigma (M,) f32 (nullable), d_color (M, n_output) f32 -> d_enc (M, 32) f32
- *   WRITTEN; g_pos / g_dir f32 parameter gradients ACCUMULATED. */
+ *   WRITTEN; g_pos / g_dir f32 parameter gradients ACCUMULATED. `workspace` is caller-
+ *   owned device memory of at least anr_ingp_field_bwd_workspace_bytes(pos, dir,
+ *   mma_dtype, M) bytes (per-wavefront f16 gradient maxima; 0 bytes for bf16, then it may
+ *   be NULL); it must not be shared with a concurrent backward launch. */
 int anr_ingp_field_supported(const anr_mlp_desc* pos, const anr_mlp_desc* dir);
 int64_t anr_ingp_field_packed_size(const anr_mlp_desc* pos, const anr_mlp_desc* dir);
 /* f16 gradient scale target of the backward (max |dL/dout| per wavefront -> 2^v);
  * returns the previous value. Test hook; process-wide. */
 int anr_ingp_field_set_grad_scale(int32_t log2_target);
-int anr_ingp_field_pack(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+int64_t anr_ingp_field_bwd_workspace_bytes(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                           int32_t mma_dtype, int64_t M);
+int anr_ingp_field_pack(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,
                         const float* pos_params, const float* dir_params, void* packed,
                         anr_stream_t stream);
-int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const void* packed,
-                       const void* enc, int64_t enc_stride, const float* dirs,
-                       int64_t n_per_ray, int64_t M, float* sigma, float* color,
-                       int64_t color_stride, anr_stream_t stream);
-int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const void* packed,
-                       const void* enc, int64_t enc_stride, const float* dirs,
-                       int64_t n_per_ray, int64_t M, const float* d_sigma,
+int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,
+                       const void* packed, const void* enc, int64_t enc_stride,
+                       const float* dirs, int64_t n_per_ray, int64_t M, float* sigma,
+                       float* color, int64_t color_stride, anr_stream_t stream);
+int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,
+                       const void* packed, const void* enc, int64_t enc_stride,
+                       const float* dirs, int64_t n_per_ray, int64_t M, const float* d_sigma,
                        const float* d_color, int64_t d_color_stride, float* d_enc,
-                       int64_t d_enc_stride, float* g_pos, float* g_dir, anr_stream_t stream);
+                       int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
+                       int64_t workspace_bytes, anr_stream_t stream);
 
 /* The same kernels over occupancy-compacted samples (anr_occupancy_compact): row r of
  * enc / d_enc is dense sample rows[r] (int32, ray-major index < n_rays * n_per_ray) of
@@ -277,16 +287,17 @@ int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, const v
  * only the listed dense rows (the caller zero-fills the rest: culled samples have
  * sigma = 0), the backward reads dL/d(sigma, color) at those rows. */
 int anr_ingp_field_fwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                            const void* packed, const void* enc, int64_t enc_stride,
-                            const float* dirs, int64_t n_per_ray, int64_t M,
-                            const int32_t* rows, float* sigma, float* color,
+                            int32_t mma_dtype, const void* packed, const void* enc,
+                            int64_t enc_stride, const float* dirs, int64_t n_per_ray,
+                            int64_t M, const int32_t* rows, float* sigma, float* color,
                             int64_t color_stride, anr_stream_t stream);
 int anr_ingp_field_bwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                            const void* packed, const void* enc, int64_t enc_stride,
-                            const float* dirs, int64_t n_per_ray, int64_t M,
-                            const int32_t* rows, const float* d_sigma, const float* d_color,
-                            int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
-                            float* g_pos, float* g_dir, anr_stream_t stream);
+                            int32_t mma_dtype, const void* packed, const void* enc,
+                            int64_t enc_stride, const float* dirs, int64_t n_per_ray,
+                            int64_t M, const int32_t* rows, const float* d_sigma,
+                            const float* d_color, int64_t d_color_stride, float* d_enc,
+                            int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
+                            int64_t workspace_bytes, anr_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Occupancy-grid sample culling (beyond the reference: BASELINE configs[4], SURVEY §8

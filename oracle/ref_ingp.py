@@ -52,7 +52,7 @@ class RefInstantNGP:
     """Parameters (float64 leaf tensors, flat per module like tcnn) + forward / loss."""
 
     def __init__(self, config: dict, state: dict, prep: dict, scale: float, max_i: float,
-                 half: bool = False):
+                 half: bool = False, mlp_half=None):
         self.cfg = config
         self.ingp = config["instant_ngp"]
         self.N = int(config["num_samples_per_ray"])
@@ -60,6 +60,9 @@ class RefInstantNGP:
         self.alt = float(config["alt_compress_factor"])
         self.prep, self.scale, self.max_i = prep, float(scale), float(max_i)
         self.half = half
+        # rounding of the per-sample pos / dir MLPs: as the rest (None) or "bf16" (the
+        # build's bf16 MFMA field, BASELINE configs[4])
+        self.mlp_half = half if mlp_half is None else mlp_half
         self.params = {m: state[m]["params"].detach().cpu().double().clone().requires_grad_(True)
                        for m in MODULES}
         self.pos_grid = _grid_cfg(self.ingp["encoding"], 3)
@@ -68,10 +71,11 @@ class RefInstantNGP:
     def _rnd(self, t):
         return t.half().double() if self.half else t
 
-    def _mlp(self, x, p, n_in, n_out, net_cfg):
+    def _mlp(self, x, p, n_in, n_out, net_cfg, half=None):
+        half = self.half if half is None else half
         y = ref_tcnn.mlp_fwd(x, p, n_in, n_out, int(net_cfg["n_neurons"]),
-                             int(net_cfg["n_hidden_layers"]), half=self.half)
-        return self._rnd(y)
+                             int(net_cfg["n_hidden_layers"]), half=half)
+        return ref_tcnn.rounder(half)(y)
 
     def forward(self, b: dict, u: torch.Tensor | None) -> dict:
         """instant_ngp.py:137-206 on a CPU ray batch; u (B, N) or None (bin midpoints)."""
@@ -82,12 +86,13 @@ class RefInstantNGP:
         pts = (pts + 1) / 2
         pts = torch.cat([pts[..., :2], pts[..., 2:] / self.alt], dim=-1)
         pos_enc = hashgrid(pts.reshape(B * N, 3), P["pos_encoder"], self.pos_grid, self._rnd)
-        pos_out = self._mlp(pos_enc, P["pos_mlp"], 32, 16, self.ingp["network"])
+        pos_out = self._mlp(pos_enc, P["pos_mlp"], 32, 16, self.ingp["network"],
+                            self.mlp_half)
         dirs = b["dir"][:, None].expand(B, N, 3).reshape(B * N, 3)
         sh = torch.from_numpy(ref_tcnn.sh(dirs.numpy(), 2))
         dir_enc = torch.cat([self._rnd(sh), pos_out[:, 1:]], dim=1)  # SH2 | Identity (19)
         color = torch.relu(self._mlp(dir_enc, P["dir_mlp"], 19, self.nb,
-                                     self.ingp["rgb_network"]))
+                                     self.ingp["rgb_network"], self.mlp_half))
         sigma = torch.relu(pos_out[:, :1])
         # surface (instant_ngp.py:143,150,173-174): normalized Cartesian x, y
         ps = (b["origin"] + b["dir"] * b["len"][:, None] + 1) / 2

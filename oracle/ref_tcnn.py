@@ -153,12 +153,23 @@ def mlp_layer_shapes(n_in, n_out, width, n_hidden):
     return shapes, nip, nop
 
 
+def rounder(half):
+    """float64 -> the kernel's 16-bit operand type -> float64 (identity for half=False)."""
+    if half == "bf16":
+        return lambda t: t.to(torch.bfloat16).double()
+    if half:
+        return lambda t: t.half().double()
+    return lambda t: t
+
+
 def mlp_fwd(x: torch.Tensor, params: torch.Tensor, n_in, n_out, width, n_hidden,
             output_relu=False, half=False) -> torch.Tensor:
     """tcnn FullyFusedMLP in float64 (autograd-capable). half=True rounds the inputs,
-    weights and every hidden activation to float16 like the f16 kernel does."""
+    weights and every hidden activation to float16 like the f16 kernel does; half="bf16"
+    rounds them to bfloat16 instead (the build's bf16 MFMA field, BASELINE configs[4],
+    which has no tcnn counterpart)."""
     shapes, nip, nop = mlp_layer_shapes(n_in, n_out, width, n_hidden)
-    rnd = (lambda t: t.half().double()) if half else (lambda t: t)
+    rnd = rounder(half)
     h = torch.ones(x.shape[0], nip, dtype=torch.float64)
     h = torch.cat([rnd(x.double()), h[:, n_in:]], dim=1)
     off = 0

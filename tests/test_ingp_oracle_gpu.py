@@ -34,7 +34,9 @@ pytestmark = pytest.mark.gpu
 IMG, BATCH, N, KS = 16, 256, 64, [0, 8]   # 8 views x 16 x 16 = 2,048 rays = 8 batches
 OPT = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
 TOL = {"f32": {"out": 1e-4, "loss": 1e-5, "grad": 2e-3},
-       "f16": {"out": 2e-2, "loss": 5e-3, "grad": 1e-1}}
+       "f16": {"out": 2e-2, "loss": 5e-3, "grad": 1e-1},
+       # bf16 field MLPs (8 significant bits, unscaled bf16 gradient tiles) over f16 tables
+       "bf16": {"out": 4e-2, "loss": 1e-2, "grad": 2e-1}}
 _REC = {}
 
 
@@ -54,15 +56,16 @@ def scene(dev):
     return SyntheticHARP2Dataset(n_views=8, img_size=IMG, device=dev, seed=0)
 
 
-def _pair(scene, dev, dtype):
+def _pair(scene, dev, dtype, mlp_dtype=None):
     from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
 
     cfg = ge._ingp_config(N)
-    p = InstantNGPPipeline(cfg, scene, dtype=dtype, fused=True, seed=5)
+    p = InstantNGPPipeline(cfg, scene, dtype=dtype, fused=True, seed=5, mlp_dtype=mlp_dtype)
     p.send_tensors_to(dev)
     pp = scene.get_point_preprocessor("horizontal")
     o = ref_ingp.RefInstantNGP(cfg, p.state_dict(), ref_ingp.prep_kwargs(pp), p.scale,
-                               scene.max_i, half=dtype == torch.float16)
+                               scene.max_i, half=dtype == torch.float16,
+                               mlp_half="bf16" if mlp_dtype == torch.bfloat16 else None)
     return p, o
 
 
@@ -71,11 +74,12 @@ def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("prec", ["f32", "f16"])
+@pytest.mark.parametrize("prec", ["f32", "f16", "bf16"])
 def test_train_step_matches_oracle(scene, dev, prec):
     from atmonr_amd.batch_loader import BatchLoader
 
-    p, o = _pair(scene, dev, torch.float32 if prec == "f32" else torch.float16)
+    p, o = _pair(scene, dev, torch.float32 if prec == "f32" else torch.float16,
+                 torch.bfloat16 if prec == "bf16" else None)
     B = 200
     batch = next(iter(BatchLoader(scene, B, seed=1)))
     u = torch.rand(B, N, generator=torch.Generator().manual_seed(2))

@@ -568,18 +568,19 @@ def test_ingp_dir_mlp_matches_unfused(dev, width, half):
     close(dparams, pr.grad, rel=rel * 2, atol=1e-8)
 
 
-def _field_ref(enc, dirs, n_per_ray, pp, pd, width, nhd, nb):
-    """sigma, color of instant_ngp.py:163-184 in float64 with the f16 kernel's roundings."""
-    pos_out = ref_tcnn.mlp_fwd(enc, pp, 32, 16, width, 1, half=True)
+def _field_ref(enc, dirs, n_per_ray, pp, pd, width, nhd, nb, half=True):
+    """sigma, color of instant_ngp.py:163-184 in float64 with the kernel's roundings
+    (half=True: f16; half="bf16": bf16 operands)."""
+    pos_out = ref_tcnn.mlp_fwd(enc, pp, 32, 16, width, 1, half=half)
     sh = torch.from_numpy(ref_tcnn.sh(dirs.detach().repeat_interleave(n_per_ray, 0).numpy(), 2))
     x = torch.cat([sh, pos_out[:, 1:]], dim=1)
-    color = ref_tcnn.mlp_fwd(x, pd, 19, nb, width, nhd, output_relu=True, half=True)
+    color = ref_tcnn.mlp_fwd(x, pd, 19, nb, width, nhd, output_relu=True, half=half)
     return torch.relu(pos_out[:, 0]), color, pos_out, x
 
 
-def _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd):
+def _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd, half=True):
     """min |pre-activation| per row over every ReLU of the field (tie detector)."""
-    h = lambda t: t.half().double()
+    h = ref_tcnn.rounder(half)
     P0 = h(pp[: 32 * width]).view(width, 32)
     P1 = h(pp[32 * width:]).view(16, width)
     a0 = h(enc) @ P0.T
@@ -598,11 +599,20 @@ def _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mma", ["f16", "bf16"])
 @pytest.mark.parametrize("width,nhd,R", [(64, 2, 29), (64, 2, 300), (32, 2, 29), (64, 1, 29),
                                          (32, 1, 31)])
-def test_ingp_field_matches_oracle(dev, width, nhd, R):
-    """anr_ingp_field_{pack,fwd,bwd} == pos MLP -> SH2|pos_out[:,1:] -> dir MLP (oracle)."""
+def test_ingp_field_matches_oracle(dev, width, nhd, R, mma):
+    """anr_ingp_field_{pack,fwd,bwd} == pos MLP -> SH2|pos_out[:,1:] -> dir MLP (oracle),
+    with the oracle rounding operands where the kernel does: f16 (the reference's tcnn
+    precision) or bf16 (BASELINE configs[4]). Tolerances (relative to the largest value):
+    f16 1e-2 forward, 2e-2 gradients; bf16 (8 significant bits, gradient tiles unscaled
+    in bf16) 2e-2 forward, 5e-2 gradients."""
     from atmonr_amd import _lib
+
+    half = "bf16" if mma == "bf16" else True
+    code = _lib.BF16 if mma == "bf16" else _lib.F16
+    rf, rb = (2e-2, 5e-2) if mma == "bf16" else (1e-2, 2e-2)
 
     nb, n_per_ray = 4, 37
     M = n_per_ray * R
@@ -618,7 +628,7 @@ def test_ingp_field_matches_oracle(dev, width, nhd, R):
     enc = torch.rand(M, 32, generator=gen) * 2 - 1
     dirs = torch.nn.functional.normalize(torch.randn(R, 3, generator=gen), dim=1)
     for _ in range(40):  # keep every ReLU input away from 0 (f16 kernel vs f64 oracle)
-        tied = _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd) < 2e-3
+        tied = _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd, half) < 2e-3
         if not tied.any():
             break
         enc[tied] = torch.rand(int(tied.sum()), 32, generator=gen) * 2 - 1
@@ -628,19 +638,19 @@ def test_ingp_field_matches_oracle(dev, width, nhd, R):
     pp_d, pd_d, enc_d, dirs_d = pp.to(dev), pd.to(dev), enc_h.to(dev), dirs.to(dev)
     packed = torch.empty(lib.anr_ingp_field_packed_size(ctypes.byref(pdsc), ctypes.byref(ddsc)),
                          device=dev, dtype=torch.float16)
-    _lib.call("anr_ingp_field_pack", ctypes.byref(pdsc), ctypes.byref(ddsc), pp_d.data_ptr(),
-              pd_d.data_ptr(), packed.data_ptr(), s)
+    _lib.call("anr_ingp_field_pack", ctypes.byref(pdsc), ctypes.byref(ddsc), code,
+              pp_d.data_ptr(), pd_d.data_ptr(), packed.data_ptr(), s)
     sigma = torch.empty(M, device=dev)
     color = torch.empty(M, nb, device=dev)
-    _lib.call("anr_ingp_field_fwd", ctypes.byref(pdsc), ctypes.byref(ddsc), packed.data_ptr(),
-              enc_d.data_ptr(), 32, dirs_d.data_ptr(), n_per_ray, M, sigma.data_ptr(),
-              color.data_ptr(), nb, s)
+    _lib.call("anr_ingp_field_fwd", ctypes.byref(pdsc), ctypes.byref(ddsc), code,
+              packed.data_ptr(), enc_d.data_ptr(), 32, dirs_d.data_ptr(), n_per_ray, M,
+              sigma.data_ptr(), color.data_ptr(), nb, s)
     e64 = enc_h.double().requires_grad_(True)
     pr_p = pp.double().requires_grad_(True)
     pr_d = pd.double().requires_grad_(True)
-    rs, rc, _, _ = _field_ref(e64, dirs, n_per_ray, pr_p, pr_d, width, nhd, nb)
-    close(sigma, rs.detach(), rel=1e-2, atol=1e-4)
-    close(color, rc.detach(), rel=1e-2, atol=1e-4)
+    rs, rc, _, _ = _field_ref(e64, dirs, n_per_ray, pr_p, pr_d, width, nhd, nb, half)
+    close(sigma, rs.detach(), rel=rf, atol=1e-4)
+    close(color, rc.detach(), rel=rf, atol=1e-4)
 
     dcol = torch.randn(M, nb, generator=gen) * 1e-2
     dsig = torch.randn(M, generator=gen) * 1e-3
@@ -649,12 +659,24 @@ def test_ingp_field_matches_oracle(dev, width, nhd, R):
     d_enc = torch.full((M, 32), float("nan"), device=dev)
     g_pos = torch.full((n_pp,), 0.5, device=dev)  # accumulated into
     g_dir = torch.full((n_pd,), -0.25, device=dev)
-    _lib.call("anr_ingp_field_bwd", ctypes.byref(pdsc), ctypes.byref(ddsc), packed.data_ptr(),
-              enc_d.data_ptr(), 32, dirs_d.data_ptr(), n_per_ray, M, dsig_d.data_ptr(),
-              dcol_d.data_ptr(), nb, d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), s)
-    close(d_enc, e64.grad, rel=2e-2, atol=1e-7)
-    close(g_pos - 0.5, pr_p.grad, rel=2e-2, atol=1e-7)
-    close(g_dir + 0.25, pr_d.grad, rel=2e-2, atol=1e-7)
+    ws_bytes = lib.anr_ingp_field_bwd_workspace_bytes(ctypes.byref(pdsc), ctypes.byref(ddsc),
+                                                      code, M)
+    assert (ws_bytes == 0) == (mma == "bf16")
+    ws = torch.empty(max(1, ws_bytes // 4), device=dev)
+    _lib.call("anr_ingp_field_bwd", ctypes.byref(pdsc), ctypes.byref(ddsc), code,
+              packed.data_ptr(), enc_d.data_ptr(), 32, dirs_d.data_ptr(), n_per_ray, M,
+              dsig_d.data_ptr(), dcol_d.data_ptr(), nb, d_enc.data_ptr(), 32, g_pos.data_ptr(),
+              g_dir.data_ptr(), ws.data_ptr() if ws_bytes else None, ws_bytes, s)
+    close(d_enc, e64.grad, rel=rb, atol=1e-7)
+    close(g_pos - 0.5, pr_p.grad, rel=rb, atol=1e-7)
+    close(g_dir + 0.25, pr_d.grad, rel=rb, atol=1e-7)
+    if mma == "f16":  # a workspace below the queried size is refused, not overrun
+        rc = lib.anr_ingp_field_bwd(ctypes.byref(pdsc), ctypes.byref(ddsc), code,
+                                    packed.data_ptr(), enc_d.data_ptr(), 32, dirs_d.data_ptr(),
+                                    n_per_ray, M, dsig_d.data_ptr(), dcol_d.data_ptr(), nb,
+                                    d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(),
+                                    ws.data_ptr(), ws_bytes - 4, s)
+        assert rc == -1 and b"workspace" in lib.anr_last_error()
 
 
 @pytest.mark.gpu
@@ -669,7 +691,10 @@ def test_ingp_field_unsupported_and_empty(dev):
                                         ctypes.byref(_lib.mlp_desc(19, 4, 64, 2, False))) == 0
     ddsc = _lib.mlp_desc(19, 4, 64, 2, False)
     rc = lib.anr_ingp_field_fwd(ctypes.byref(pdsc), ctypes.byref(_lib.mlp_desc(19, 4, 64, 3, False)),
-                                None, None, 32, None, 1, 10, None, None, 4, None)
+                                _lib.F16, None, None, 32, None, 1, 10, None, None, 4, None)
     assert rc == -1 and b"unsupported" in lib.anr_last_error()
-    assert lib.anr_ingp_field_fwd(ctypes.byref(pdsc), ctypes.byref(ddsc), None, None, 32, None,
-                                  1, 0, None, None, 4, None) == 0
+    rc = lib.anr_ingp_field_fwd(ctypes.byref(pdsc), ctypes.byref(ddsc), _lib.F32, None, None, 32,
+                                None, 1, 10, None, None, 4, None)
+    assert rc == -1 and b"mma_dtype" in lib.anr_last_error()
+    assert lib.anr_ingp_field_fwd(ctypes.byref(pdsc), ctypes.byref(ddsc), _lib.F16, None, None,
+                                  32, None, 1, 0, None, None, 4, None) == 0

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--width", type=int, default=64)
     ap.add_argument("--nhd", type=int, default=2)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--bf16", action="store_true", help="bf16 MFMA operands (configs[4])")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -50,19 +51,22 @@ def main():
     d_enc = torch.empty(M, 32, device=dev)
     g_pos = torch.zeros_like(pp)
     g_dir = torch.zeros_like(pdir)
+    code = _lib.BF16 if args.bf16 else _lib.F16
+    ws_bytes = lib.anr_ingp_field_bwd_workspace_bytes(pdesc, ddesc, code, M)
+    ws = torch.empty(max(1, ws_bytes // 4), device=dev)
     s = _lib.stream(dev)
     timer = _lib.KernelTimer()
     with timer:
         for _ in range(args.iters):
-            _lib.call("anr_ingp_field_pack", pdesc, ddesc, pp.data_ptr(), pdir.data_ptr(),
-                      packed.data_ptr(), s, tag="pack")
-            _lib.call("anr_ingp_field_fwd", pdesc, ddesc, packed.data_ptr(), enc.data_ptr(), 32,
-                      dirs.data_ptr(), args.samples, M, sigma.data_ptr(), color.data_ptr(), 4,
-                      s, tag="field_fwd")
-            _lib.call("anr_ingp_field_bwd", pdesc, ddesc, packed.data_ptr(), enc.data_ptr(), 32,
-                      dirs.data_ptr(), args.samples, M, dsig.data_ptr(), dcol.data_ptr(), 4,
-                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), s,
-                      tag="field_bwd")
+            _lib.call("anr_ingp_field_pack", pdesc, ddesc, code, pp.data_ptr(),
+                      pdir.data_ptr(), packed.data_ptr(), s, tag="pack")
+            _lib.call("anr_ingp_field_fwd", pdesc, ddesc, code, packed.data_ptr(),
+                      enc.data_ptr(), 32, dirs.data_ptr(), args.samples, M, sigma.data_ptr(),
+                      color.data_ptr(), 4, s, tag="field_fwd")
+            _lib.call("anr_ingp_field_bwd", pdesc, ddesc, code, packed.data_ptr(),
+                      enc.data_ptr(), 32, dirs.data_ptr(), args.samples, M, dsig.data_ptr(),
+                      dcol.data_ptr(), 4, d_enc.data_ptr(), 32, g_pos.data_ptr(),
+                      g_dir.data_ptr(), ws.data_ptr(), ws_bytes, s, tag="field_bwd")
     torch.cuda.synchronize()
     for k, v in timer.summary().items():
         print(f"{k:12s} avg {v['avg_ms']:.4f} ms  ({v['launches']} calls)")

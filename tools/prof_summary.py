@@ -27,8 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAGS = {
     "hash_fwd": "hashgrid_fwd_kernel<3, 2, __half, __half>",
     "hash_bwd": "hashgrid_bwd_v2_kernel<3, float>",
-    "field_fwd": "field::fwd_kernel<64, 2, false>",
-    "field_bwd": "field::bwd_kernel<64, 2, true, false>",
+    "field_fwd": "field::fwd_kernel<64, 2, false, false>",
+    "field_bwd": "field::bwd_kernel<64, 2, true, false, false>",
     "composite_fwd": "rb::fwd_kernel<float, 4, 1, 4>",
     "composite_bwd": "rb::bwd_kernel<float, 4, 1, 4>",
     "sampler": "sample_uniform_bins_kernel",
@@ -36,10 +36,18 @@ TAGS = {
 
 
 def per_launch(path: str) -> dict[str, float]:
+    """Median per launch over the second half of each kernel's launches: the bench
+    network is dead for its first few AdamW steps (tools/liveness.py: no densities, no
+    hash-grid gradients, the backward's atomics skipped), so early launches are not the
+    steady state the timed region measures."""
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+    out = {}
+    for k, v in agg.items():
+        tail = sorted(v[len(v) // 2:])
+        out[k] = tail[len(tail) // 2]
+    return out
 
 
 def main(src: str, tag: str, key_suffix: str = "baseline:8192x1024"):
@@ -56,27 +64,46 @@ def main(src: str, tag: str, key_suffix: str = "baseline:8192x1024"):
              "`rocprofv3 --kernel-trace --stats` plus separate `--pmc FETCH_SIZE` and "
              "`--pmc WRITE_SIZE` passes (tools/prof.sh). Traffic = (2*FETCH_SIZE + "
              "WRITE_SIZE) KiB per launch (gfx950 FETCH_SIZE half-count correction).", "",
-             "| kernel | calls | avg us | % time | HBM traffic / launch (MB) |",
-             "|---|---|---|---|---|"]
+             "Steady avg = mean duration over the second half of each kernel's launches in "
+             "the kernel trace (the bench network is alive from step ~7; the first steps' "
+             "backward skips its zero-gradient atomics).", "",
+             "| kernel | calls | avg us | steady avg us | % time | HBM traffic / launch (MB) |",
+             "|---|---|---|---|---|---|"]
+    steady = {}
+    tpath = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tpath):
+        durs = collections.defaultdict(list)
+        for r in csv.DictReader(open(tpath)):
+            durs[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        for k, v in durs.items():
+            tail = v[len(v) // 2:]
+            steady[k] = sum(tail) / len(tail) / 1e3
     for r in rows[:25]:
         name = r["Name"]
         f = next((v for k, v in fetch.items() if k == name or k.startswith(name[:80])), None)
         w = next((v for k, v in write.items() if k == name or k.startswith(name[:80])), None)
         traffic = (2 * f + w) * 1024 / 1e6 if f is not None and w is not None else None
         short = name.replace("|", "/")[:90]
+        sa = next((v for k, v in steady.items() if k == name or k.startswith(name[:80])), None)
         lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
-                     f"{float(r['Percentage']):.1f} | "
+                     f"{'' if sa is None else f'{sa:.1f}'} | {float(r['Percentage']):.1f} | "
                      f"{'' if traffic is None else f'{traffic:.1f}'} |")
+    apath = os.path.join(src, "atomic", "run_counter_collection.csv")
+    atomic = per_launch(apath) if os.path.exists(apath) else {}
     for t, pat in TAGS.items():
         f = next((v for k, v in fetch.items() if pat in k), None)
         w = next((v for k, v in write.items() if pat in k), None)
+        a = next((v for k, v in atomic.items() if pat in k), None)
         if f is not None and w is not None:
-            pmc[f"{t}:{key_suffix}"] = {"bytes": round((2 * f + w) * 1024),
-                                        "fetch_kib": round(f, 1), "write_kib": round(w, 1)}
+            ent = {"bytes": round((2 * f + w) * 1024), "fetch_kib": round(f, 1),
+                   "write_kib": round(w, 1), "source": tag}
+            if a:  # TCC_EA0_ATOMIC_sum: memory-side atomic requests (64-B segments)
+                ent["atomic_requests"] = round(a)
+            pmc[f"{t}:{key_suffix}"] = ent
     json.dump(pmc, open(pmc_path, "w"), indent=1, sort_keys=True)
     open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *sys.argv[3:4])

@@ -1,0 +1,161 @@
+// Microbenchmarks that MEASURE the MI355X ceilings the hot-path rooflines are priced
+// against: spec sheets are not peaks.
+//
+//   ub_copy     float4 stream copy            -> HBM GB/s (read + written bytes)
+//   ub_read     float4 stream read (reduce)   -> HBM GB/s (read bytes)
+//   ub_mfma     back-to-back 16x16x32 f16 / bf16 MFMAs on random operands, every SIMD
+//               -> dense TFLOP/s
+//   ub_atomic   no-return global_atomic_add_f32 wave-instructions cut into segments of
+//               `seg_lanes` consecutive dwords, each segment at an independent random,
+//               segment-aligned address of a `n_floats` table -> segment requests/s.
+//               seg_lanes = 4 with 16 segments per instruction is the hash-grid
+//               backward's shape (hashgrid.hip v2: lane = 4*level + 2*xbit + feature).
+//
+// Test/measurement infrastructure, not product: built to tools/ubench/libanr_ubench.so
+// by __graft_entry__.build(); bench.py loads it in its untimed phase. Plain C ABI
+// (device pointers, sizes, a hipStream_t), int status.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(256) copy_kernel(const float4* __restrict__ src,
+                                                   float4* __restrict__ dst, int64_t n) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {  // 4 independent loads in flight
+    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) read_kernel(const float4* __restrict__ src, int64_t n,
+                                                   float* __restrict__ sink) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float acc = 0.f;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    acc += (a.x + b.y) + (c.z + d.w);
+  }
+  for (; i < n; i += stride) acc += src[i].x;
+  if (acc == 1234.5f) sink[threadIdx.x] = acc;  // never true on the bench data; keeps loads
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {  // lowbias32 integer hash
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+template <bool BF16>
+__global__ void __launch_bounds__(256) mfma_kernel(int iters, float* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  // random operands (zeros would let the chip hold a higher clock: MICROARCH DVFS notes)
+  h8 ah, bh;
+  b8 ab, bb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float va = (float)(mix32(t * 16 + j) & 0xffff) * (1.f / 65536.f) - 0.5f;
+    float vb = (float)(mix32(t * 16 + 8 + j) & 0xffff) * (1.f / 65536.f) - 0.5f;
+    ah[j] = (_Float16)va;
+    bh[j] = (_Float16)vb;
+    ab[j] = (__bf16)va;
+    bb[j] = (__bf16)vb;
+  }
+  f4 c0 = {0, 0, 0, 0}, c1 = {1, 1, 1, 1}, c2 = {2, 2, 2, 2}, c3 = {3, 3, 3, 3};
+  for (int i = 0; i < iters; ++i) {
+    if constexpr (BF16) {
+      c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, c3, 0, 0, 0);
+    } else {
+      c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c3, 0, 0, 0);
+    }
+  }
+  f4 s = c0 + c1 + c2 + c3;
+  out[t] = s[0] + s[1] + s[2] + s[3];
+}
+
+// f32-input MFMA (v_mfma_f32_16x16x4_f32: 2*16*16*4 FLOP), the NeRF MLP's GEMM precision
+__global__ void __launch_bounds__(256) mfma_f32_kernel(int iters, float* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const float a = (float)(mix32(t) & 0xffff) * (1.f / 65536.f) - 0.5f;
+  const float b = (float)(mix32(t + 7) & 0xffff) * (1.f / 65536.f) - 0.5f;
+  f4 c0 = {0, 0, 0, 0}, c1 = {1, 1, 1, 1}, c2 = {2, 2, 2, 2}, c3 = {3, 3, 3, 3};
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c3, 0, 0, 0);
+  }
+  f4 s = c0 + c1 + c2 + c3;
+  out[t] = s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ void __launch_bounds__(256) atomic_kernel(float* __restrict__ table, int64_t n_seg,
+                                                     int seg_lanes, int iters, uint32_t seed) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int seg = lane / seg_lanes, j = lane - seg * seg_lanes;
+  for (int i = 0; i < iters; ++i) {
+    uint32_t h = mix32(seed ^ mix32(wave * 0x9E3779B9U + i * 131u + seg));
+    int64_t s = (int64_t)(((uint64_t)h * (uint64_t)n_seg) >> 32);
+    __hip_atomic_fetch_add(table + s * seg_lanes + j, 1.0f, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+extern "C" {
+
+int ub_copy(const void* src, void* dst, int64_t n_float4, int blocks, void* stream) {
+  if (n_float4 <= 0 || blocks <= 0) return 1;
+  copy_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((const float4*)src, (float4*)dst,
+                                                      n_float4);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int ub_read(const void* src, int64_t n_float4, float* sink, int blocks, void* stream) {
+  if (n_float4 <= 0 || blocks <= 0) return 1;
+  read_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((const float4*)src, n_float4, sink);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// kind 0 f16, 1 bf16, 2 f32. out: blocks*256 floats. FLOPs = blocks * 4 waves * iters * 4 *
+// (2*16*16*32) for f16/bf16, (2*16*16*4) for f32.
+int ub_mfma(int bf16, int iters, int blocks, float* out, void* stream) {
+  if (iters <= 0 || blocks <= 0) return 1;
+  if (bf16 == 2)
+    mfma_f32_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(iters, out);
+  else if (bf16)
+    mfma_kernel<true><<<blocks, 256, 0, (hipStream_t)stream>>>(iters, out);
+  else
+    mfma_kernel<false><<<blocks, 256, 0, (hipStream_t)stream>>>(iters, out);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Segment requests = blocks * 4 waves * iters * (64 / seg_lanes).
+int ub_atomic(float* table, int64_t n_floats, int seg_lanes, int iters, int blocks,
+              uint32_t seed, void* stream) {
+  if (seg_lanes <= 0 || 64 % seg_lanes || n_floats < seg_lanes || iters <= 0 || blocks <= 0)
+    return 1;
+  atomic_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(table, n_floats / seg_lanes, seg_lanes,
+                                                         iters, seed);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // extern "C"

@@ -19,6 +19,23 @@ Restates src/atmonr/pipelines/instant_ngp.py:137-206 (forward) and :249-263
 and hidden activations, the f16 MLP outputs) so the oracle tracks the bench
 configuration; gradients pass through the roundings unchanged (casts are identity in
 autograd). tcnn semantics are unpinned against real tinycudann (see ref_tcnn).
+
+``semantics="reference"`` (with ``half=True``) restates what the REFERENCE computes in
+its f16 Instant-NGP path, as opposed to what this build computes:
+
+* every tinycudann module returns an f16 tensor, and its backward follows tcnn's
+  torch binding (tinycudann/modules.py, upstream; not in /root/reference): the incoming
+  f16 gradient is multiplied by loss_scale = 128 in f16, the module's backward runs on
+  f16 tiles (hidden-layer gradients rounded to f16 here), the parameter gradient comes
+  back in f16 and is divided by 128, the input gradient likewise;
+* the composite (graphics_utils.py:6-77) runs on those f16 tensors: z is cast to f16
+  km (graphics_utils.py:28), alpha, the cumprod and the sums are f16 torch ops (f32
+  accumulation inside the scan and sums, as torch does on both CPU and GPU);
+* the loss takes the f16 prediction and the target cast to f16 (instant_ngp.py:262);
+  the f16 autograd of the composite and loss rounds every gradient to f16.
+Approximations (tcnn absent): the MLP backward's rounding is applied per layer, not per
+16x16 tile; the hash-grid gradient (tcnn: f16 half2 atomics) is summed in f64 and
+rounded once.
 """
 
 from __future__ import annotations
@@ -48,11 +65,55 @@ def hashgrid(x: torch.Tensor, table: torch.Tensor, cfg, rnd) -> torch.Tensor:
     return rnd(torch.cat(outs, dim=1))
 
 
+LOSS_SCALE = 128.0  # tinycudann.modules default loss scale for f16 parameters
+
+
+class _RoundBoth(torch.autograd.Function):
+    """x -> f16(x) forward, g -> f16(g) backward (values and gradients on f16 tiles)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.half().double()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.half().double()
+
+
+class _TcnnCall(torch.autograd.Function):
+    """One tinycudann module call in reference semantics: f16 output; backward with the
+    f16 gradient scaled by LOSS_SCALE, the f64 module graph run on it, parameter and input
+    gradients rounded to f16 and unscaled."""
+
+    @staticmethod
+    def forward(ctx, x, params, fn):
+        with torch.enable_grad():
+            x64 = x.detach().double().requires_grad_(x.requires_grad)
+            p64 = params.detach().double().requires_grad_(True)
+            y = fn(x64, p64)
+        ctx.graph = (x64, p64, y)
+        ctx.x_dtype = x.dtype
+        return y.detach().half()
+
+    @staticmethod
+    def backward(ctx, g):
+        x64, p64, y = ctx.graph
+        gs = (g.float() * LOSS_SCALE).half().double()
+        ins = (x64, p64) if x64.requires_grad else (p64,)
+        grads = torch.autograd.grad(y, ins, gs, allow_unused=True)
+        gp = grads[-1]
+        gp = torch.zeros_like(p64) if gp is None else gp.half().double() / LOSS_SCALE
+        gx = None
+        if x64.requires_grad and grads[0] is not None:
+            gx = (grads[0].half().double() / LOSS_SCALE).to(ctx.x_dtype)
+        return gx, gp, None
+
+
 class RefInstantNGP:
     """Parameters (float64 leaf tensors, flat per module like tcnn) + forward / loss."""
 
     def __init__(self, config: dict, state: dict, prep: dict, scale: float, max_i: float,
-                 half: bool = False, mlp_half=None):
+                 half: bool = False, mlp_half=None, semantics: str = "build"):
         self.cfg = config
         self.ingp = config["instant_ngp"]
         self.N = int(config["num_samples_per_ray"])
@@ -63,6 +124,9 @@ class RefInstantNGP:
         # rounding of the per-sample pos / dir MLPs: as the rest (None) or "bf16" (the
         # build's bf16 MFMA field, BASELINE configs[4])
         self.mlp_half = half if mlp_half is None else mlp_half
+        if semantics not in ("build", "reference") or (semantics == "reference" and half is not True):
+            raise ValueError("semantics='reference' is the reference's f16 path (half=True)")
+        self.semantics = semantics
         self.params = {m: state[m]["params"].detach().cpu().double().clone().requires_grad_(True)
                        for m in MODULES}
         self.pos_grid = _grid_cfg(self.ingp["encoding"], 3)
@@ -79,6 +143,8 @@ class RefInstantNGP:
 
     def forward(self, b: dict, u: torch.Tensor | None) -> dict:
         """instant_ngp.py:137-206 on a CPU ray batch; u (B, N) or None (bin midpoints)."""
+        if self.semantics == "reference":
+            return self._forward_reference(b, u)
         P = self.params
         B, N = b["origin"].shape[0], self.N
         pts, z = ref_path.sample_uniform_bins(b["origin"], b["dir"], b["len"], u=u, n_bins=N)
@@ -112,10 +178,74 @@ class RefInstantNGP:
                 "color_fine": color.view(B, N, -1)[:, :-1],
                 "sigma_fine": sigma.view(B, N, 1)[:, :-1], "color_surf": color_surf}
 
+    # ------------------------------------------------------------ reference semantics
+    def _mlp_ref(self, x, p, n_in, n_out, net_cfg):
+        """FullyFusedMLP on f16 tiles: weights, activations and their gradients in f16."""
+        shapes, nip, _ = ref_tcnn.mlp_layer_shapes(n_in, n_out, int(net_cfg["n_neurons"]),
+                                                   int(net_cfg["n_hidden_layers"]))
+        h = torch.cat([_RoundBoth.apply(x),
+                       torch.ones(x.shape[0], nip - n_in, dtype=torch.float64)], dim=1)
+        off = 0
+        for k, (o, i) in enumerate(shapes):
+            W = p[off:off + o * i].half().double().view(o, i)
+            off += o * i
+            h = h @ W.t()
+            if k < len(shapes) - 1:
+                h = _RoundBoth.apply(torch.relu(h))
+        return h[:, :n_out]
+
+    def _grid_ref(self, cfg):
+        def fn(x, p):
+            return hashgrid(x, p, cfg, lambda t: t.half().double())
+        return fn
+
+    def _forward_reference(self, b: dict, u) -> dict:
+        P = self.params
+        B, N = b["origin"].shape[0], self.N
+        pts, z = ref_path.sample_uniform_bins(b["origin"], b["dir"], b["len"], u=u, n_bins=N)
+        pts = ref_nerf.preprocess_torch(pts, **self.prep)
+        pts = (pts + 1) / 2
+        pts = torch.cat([pts[..., :2], pts[..., 2:] / self.alt], dim=-1).float()
+        ing = self.ingp
+        pos_enc = _TcnnCall.apply(pts.reshape(B * N, 3), P["pos_encoder"],
+                                  self._grid_ref(self.pos_grid))
+        pos_out = _TcnnCall.apply(pos_enc, P["pos_mlp"], lambda x, p: self._mlp_ref(
+            x, p, 32, 16, ing["network"]))
+        dirs = b["dir"][:, None].expand(B, N, 3).reshape(B * N, 3).float()
+        # dir_encoder(cat[dirs, pos_out[:, 1:]]): the cat promotes to f32 (instant_ngp.py:
+        # 165-169); SH2 | Identity, f16 output; the identity part passes the gradient
+        x_dir = torch.cat([dirs, pos_out[:, 1:]], dim=1)
+
+        def dir_enc_fn(x, p):
+            sh = _sh2(x[:, :3])
+            return torch.cat([sh, x[:, 3:]], dim=1) + 0.0 * p.sum()
+        dir_enc = _TcnnCall.apply(x_dir, torch.zeros(1, dtype=torch.float64), dir_enc_fn)
+        color = _TcnnCall.apply(dir_enc, P["dir_mlp"], lambda x, p: self._mlp_ref(
+            x, p, 19, self.nb, ing["rgb_network"]))
+        ps = ((b["origin"] + b["dir"] * b["len"][:, None] + 1) / 2).float()
+        surf_in = torch.cat([ps[:, :2], b["dir"].float()], dim=1)
+        surf_grid = self._grid_ref(self.surf_grid)
+
+        def surf_enc_fn(x, p):
+            return torch.cat([surf_grid(x[:, :2], p), _sh2(x[:, 2:5])], dim=1)
+        surf_enc = _TcnnCall.apply(surf_in, P["surf_encoder"], surf_enc_fn)
+        color_surf = _TcnnCall.apply(surf_enc, P["surf_mlp"], lambda x, p: self._mlp_ref(
+            x, p, 36, self.nb, ing["surface_network"]))
+        color = torch.relu(color.view(B, N, -1))
+        color_surf = torch.relu(color_surf)
+        sigma = torch.relu(pos_out[:, :1]).view(B, N, 1)
+        cm, alpha, weights, atmo, surf = ref_path.render_with_surface(
+            z * (self.scale / 1000), color, sigma, color_surf)  # f16 (z cast inside)
+        return {"color_map_fine": cm, "color_map_atmo": atmo, "color_map_surf": surf,
+                "weights_fine": weights, "z_vals_fine": z, "color_fine": color[:, :-1],
+                "sigma_fine": sigma[:, :-1], "color_surf": color_surf}
+
     def loss(self, b: dict, res: dict, name: str = "mse_plus_hdr") -> torch.Tensor:
-        """instant_ngp.py:249-263: loss_fn(take_along_dim(color_map, irgb), rad, max_i)."""
+        """instant_ngp.py:249-263: loss_fn(take_along_dim(color_map, irgb), rad, max_i)
+        (the target cast to the prediction's dtype, :262)."""
         pred = torch.take_along_dim(res["color_map_fine"], b["irgb_idx"][:, None], 1)[:, 0]
-        return ref_path.LOSSES[name](pred, b["rad"].double(), self.max_i)
+        gt = b["rad"].to(pred.dtype) if pred.dtype == torch.float16 else b["rad"].double()
+        return ref_path.LOSSES[name](pred, gt, self.max_i)
 
     def optimizer(self, opt_cfg: dict) -> torch.optim.Optimizer:
         """AdamW, weight decay on the MLPs only (instant_ngp.py:107-127)."""
@@ -125,6 +255,14 @@ class RefInstantNGP:
                    "weight_decay": opt_cfg["weight_decay"]}]
         return torch.optim.AdamW(groups, lr=opt_cfg["lr"], betas=tuple(opt_cfg["betas"]),
                                  eps=opt_cfg["eps"])
+
+
+def _sh2(d: torch.Tensor) -> torch.Tensor:
+    """tcnn SphericalHarmonics degree 2 on x in [0,1]^3 (remapped 2x-1), differentiable."""
+    x = d * 2.0 - 1.0
+    c1 = 0.48860251190291987
+    return torch.stack([torch.full_like(x[:, 0], 0.28209479177387814), -c1 * x[:, 1],
+                        c1 * x[:, 2], -c1 * x[:, 0]], dim=1)
 
 
 def cpu_batch(b: dict) -> dict:

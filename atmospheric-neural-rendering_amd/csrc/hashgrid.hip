@@ -735,6 +735,62 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v2_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Forward v4 (F = 2): one thread per SAMPLE, looping over the levels, tiny-cuda-nn's
+// decomposition with gfx950's wave64 (64 consecutive samples of one ray per wavefront).
+// Every level's 2^D corners are gathered for every sample: on the coarse levels all
+// lanes of a wavefront read the same few lines (one L1 lookup serves them), on the fine
+// levels the gathers of the wavefront's ~17 distinct cells per level go out together.
+// Unlike the walkers (v1-v3) there is no data-dependent branch: the per-sample work is
+// one straight unrolled stream of index math, gathers and FMAs, and the compiler keeps
+// several levels' gathers in flight. Same corner order and fma chain as v1, so the
+// results are bit-identical to it.
+template <int D, typename TT, typename TO, int NL>
+__global__ void __launch_bounds__(256) hashgrid_fwd_v4_kernel(
+    GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
+    const TT* __restrict__ table, TO* __restrict__ out, int64_t out_stride) {
+  const int64_t m = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float xv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) xv[d] = x[m * x_stride + d];
+  TO* __restrict__ orow = out + m * out_stride;
+#pragma unroll
+  for (int level = 0; level < NL; ++level) {
+    if (level >= n_levels) continue;  // (continue, not break: keeps the loop unrollable)
+    const float scale = G.scale[level];
+    LevelIdx<D> li;
+    li.init(G.size[level], G.res[level]);
+    const TT* __restrict__ grid = table + static_cast<int64_t>(G.offset[level]) * 2;
+    float w[D];
+    uint32_t g[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float p = fmaf(scale, xv[d], 0.5f);
+      const float fl = floorf(p);
+      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
+      w[d] = p - fl;
+    }
+    uint32_t idx[1 << D];
+    cell_corners<D>(li, g, idx);
+    typename RawF2<TT>::type raw[1 << D];
+#pragma unroll
+    for (int c = 0; c < (1 << D); ++c) raw[c] = RawF2<TT>::load(grid + static_cast<int64_t>(idx[c]) * 2);
+    float acc[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < (1 << D); ++c) {
+      float wt = 1.0f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
+      float v[2];
+      RawF2<TT>::unpack(raw[c], v);
+      acc[0] = fmaf(wt, v[0], acc[0]);
+      acc[1] = fmaf(wt, v[1], acc[1]);
+    }
+    store_feat<TO, 2>(orow + level * 2, acc);
+  }
+}
+
 template <int D, typename TG>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
@@ -886,10 +942,11 @@ static int64_t pick_chunk_v2(int64_t M) {
 // bound by the rate of cache-line fetches its gathers cause, not by their latency.
 static int g_hashgrid_mode = [] {
   const char* e = getenv("ANR_HASHGRID_MODE");
-  return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
+  return (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 0;
 }();
 static bool fwd_v2() { return g_hashgrid_mode == 2; }
 static bool fwd_v3() { return g_hashgrid_mode == 3; }
+static bool fwd_v4() { return g_hashgrid_mode == 4; }
 static bool bwd_v2() { return g_hashgrid_mode != 1; }
 
 // Levels per wavefront of the forward walker (1, 2, 4, 8, 16, 32 or 64).
@@ -932,6 +989,20 @@ static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
     else ANR_HG_FWD2(float, float);
 #undef ANR_HG_FWD2
     ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v2)");
+    return ANR_OK;
+  }
+  if (F == 2 && d->n_levels <= 16 && fwd_v4()) {
+    const dim3 grid(static_cast<unsigned>(ceil_div(M, 256))), block(256);
+#define ANR_HG_FWD4(TT, TO)                                                                  \
+  hipLaunchKernelGGL((hashgrid_fwd_v4_kernel<D, TT, TO, 16>), grid, block, 0, s, G,          \
+                     d->n_levels, x, x_stride, M, static_cast<const TT*>(table),             \
+                     static_cast<TO*>(out), out_stride)
+    if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD4(__half, __half);
+    else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD4(__half, float);
+    else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD4(float, __half);
+    else ANR_HG_FWD4(float, float);
+#undef ANR_HG_FWD4
+    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v4)");
     return ANR_OK;
   }
   const int lpw = fwd_lpw();
@@ -1006,7 +1077,7 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 
 extern "C" int anr_hashgrid_force_v1(int32_t mode) {
   const int prev = anr::g_hashgrid_mode;
-  anr::g_hashgrid_mode = (mode >= 0 && mode <= 3) ? mode : 0;
+  anr::g_hashgrid_mode = (mode >= 0 && mode <= 4) ? mode : 0;
   return prev;
 }
 

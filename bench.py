@@ -278,7 +278,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spec-peaks", action="store_true",
                     help="price the rooflines against spec-sheet peaks instead of measuring")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-budget", type=float, default=40.0)
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--occupancy", action="store_true",
                     help="BASELINE configs[4]: occupancy-grid culling (beyond the reference); "

@@ -791,6 +791,139 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v4_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Forward v5 (F = 2, f16 table): v1's walker (one lane per (chunk, level), corners of
+// the current cell kept in registers) with the corner gathers COMPACTED across the
+// wavefront. In v1 a wavefront of 16 levels x 4 chunks executes its 2^D gather
+// instructions on nearly every sample, because almost always some lane enters a new
+// cell, while on average only ~5 of the 64 lanes do: the texture addresser, not the
+// memory system, bounds it (TA busy 85 % of the kernel; profiles/r02_sq_bench.txt).
+// Here the lanes that enter a new cell write their 2^D corner indices to a per-wave LDS
+// list; the wave then gathers the list densely, 64 corners per instruction (usually
+// one instruction for all of them), writes the values back to the list, and each lane
+// reads its own 2^D. Same corner values and the same fma chain as v1: bit-identical.
+template <int D, typename TO>
+__global__ void __launch_bounds__(256) hashgrid_fwd_v5_kernel(
+    GridLevels G, int n_levels, int lpw, int n_groups, const float* __restrict__ x,
+    int64_t x_stride, int64_t M, int64_t K, const __half* __restrict__ table,
+    TO* __restrict__ out, int64_t out_stride) {
+  constexpr int NC = 1 << D;
+  __shared__ uint32_t list[4][64 * NC];  // per wave: corner entry index, then its value
+  const int lane = static_cast<int>(threadIdx.x & 63);
+  const int wv = static_cast<int>(threadIdx.x >> 6);
+  uint32_t* __restrict__ L = list[wv];
+  const int lg = static_cast<int>(blockIdx.x % n_groups);
+  const int64_t wave_in = (static_cast<int64_t>(blockIdx.x / n_groups) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t chunk = wave_in * (64 / lpw) + lane / lpw;
+  const int level_raw = lg * lpw + lane % lpw;
+  const int64_t m0 = chunk * K;
+  const bool lane_ok = level_raw < n_levels && m0 < M;
+  const int level = lane_ok ? level_raw : 0;  // inactive lanes still take part in the wave
+  const int64_t m1 = lane_ok ? (m0 + K < M ? m0 + K : M) : m0;
+  const uint32_t* __restrict__ tab = reinterpret_cast<const uint32_t*>(table);  // f16 pairs
+
+  const float scale = G.scale[level];
+  const uint32_t off = G.offset[level];
+  LevelIdx<D> li;
+  li.init(G.size[level], G.res[level]);
+
+  uint32_t cell[D];
+  bool have = false;
+#pragma unroll
+  for (int d = 0; d < D; ++d) cell[d] = 0u;
+  uint32_t raw[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) raw[c] = 0u;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  auto step = [&](int64_t m, const float* xv, bool act) {
+    float w[D];
+    uint32_t g[D];
+    bool same = have;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float p = fmaf(scale, xv[d], 0.5f);
+      const float fl = floorf(p);
+      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
+      w[d] = p - fl;
+      same = same && (g[d] == cell[d]);
+    }
+    const bool changed = act && !same;
+    const uint64_t mask = __ballot(changed);
+    if (mask != 0ull) {  // wave-uniform
+      const int rank = __popcll(mask & below);
+      if (changed) {
+        uint32_t idx[NC];
+        cell_corners<D>(li, g, idx);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) L[rank * NC + c] = off + idx[c];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int total = __popcll(mask) * NC;
+      for (int b = 0; b < total; b += 64) {  // usually one pass
+        const int k = b + lane;
+        if (k < total) L[k] = tab[L[k]];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (changed) {
+        have = true;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) raw[c] = L[rank * NC + c];
+#pragma unroll
+        for (int d = 0; d < D; ++d) cell[d] = g[d];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (!act) return;
+    float acc[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float wt = 1.0f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
+      float v[2];
+      RawF2<__half>::unpack(raw[c], v);
+      acc[0] = fmaf(wt, v[0], acc[0]);
+      acc[1] = fmaf(wt, v[1], acc[1]);
+    }
+    store_feat<TO, 2>(out + m * out_stride + level * 2, acc);
+  };
+
+  // coordinates prefetched one batch ahead (indices clamped: no branch around the loads);
+  // the loop runs the wave's longest chunk (K samples) on every lane
+  constexpr int BS = HASH_FBS;
+  float xb[BS][D], xn[BS][D];
+  const int64_t mlast = m1 > m0 ? m1 - 1 : m0;
+  auto load_batch = [&](int64_t mb, float (*xo)[D]) {
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      int64_t mm = mb + j < m1 ? mb + j : mlast;
+      if (mm >= M) mm = M - 1;
+#pragma unroll
+      for (int d = 0; d < D; ++d) xo[j][d] = x[mm * x_stride + d];
+    }
+  };
+  load_batch(m0, xb);
+  for (int64_t jb = 0; jb < K; jb += BS) {
+    load_batch(m0 + jb + BS, xn);
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      const int64_t m = m0 + jb + j;
+      step(m, xb[j], jb + j < K && m < m1);
+    }
+#pragma unroll
+    for (int j = 0; j < BS; ++j)
+#pragma unroll
+      for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
+  }
+}
+
 template <int D, typename TG>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
@@ -942,11 +1075,12 @@ static int64_t pick_chunk_v2(int64_t M) {
 // bound by the rate of cache-line fetches its gathers cause, not by their latency.
 static int g_hashgrid_mode = [] {
   const char* e = getenv("ANR_HASHGRID_MODE");
-  return (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 0;
+  return (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 0;
 }();
 static bool fwd_v2() { return g_hashgrid_mode == 2; }
 static bool fwd_v3() { return g_hashgrid_mode == 3; }
 static bool fwd_v4() { return g_hashgrid_mode == 4; }
+static bool fwd_v5() { return g_hashgrid_mode == 5; }
 static bool bwd_v2() { return g_hashgrid_mode != 1; }
 
 // Levels per wavefront of the forward walker (1, 2, 4, 8, 16, 32 or 64).
@@ -1011,6 +1145,18 @@ static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
   const int64_t chunks = ceil_div(M, K);
   const int64_t blocks_per_group = ceil_div(ceil_div(chunks, 64 / lpw), 4);
   const dim3 grid(static_cast<unsigned>(blocks_per_group * n_groups)), block(256);
+  if (F == 2 && fwd_v5() && tdt == ANR_F16) {
+    if (odt == ANR_F16)
+      hipLaunchKernelGGL((hashgrid_fwd_v5_kernel<D, __half>), grid, block, 0, s, G, d->n_levels,
+                         lpw, n_groups, x, x_stride, M, K, static_cast<const __half*>(table),
+                         static_cast<__half*>(out), out_stride);
+    else
+      hipLaunchKernelGGL((hashgrid_fwd_v5_kernel<D, float>), grid, block, 0, s, G, d->n_levels,
+                         lpw, n_groups, x, x_stride, M, K, static_cast<const __half*>(table),
+                         static_cast<float*>(out), out_stride);
+    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v5)");
+    return ANR_OK;
+  }
   if (F == 2 && fwd_v3()) {
 #define ANR_HG_FWD3(TT, TO, BS)                                                             \
   hipLaunchKernelGGL((hashgrid_fwd_v3_kernel<D, TT, TO, BS>), grid, block, 0, s, G,         \
@@ -1077,7 +1223,7 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 
 extern "C" int anr_hashgrid_force_v1(int32_t mode) {
   const int prev = anr::g_hashgrid_mode;
-  anr::g_hashgrid_mode = (mode >= 0 && mode <= 4) ? mode : 0;
+  anr::g_hashgrid_mode = (mode >= 0 && mode <= 5) ? mode : 0;
   return prev;
 }
 

@@ -136,10 +136,10 @@ def _grid_inputs(dev, cfg, M, coherent, seed=0):
 # hash-grid kernel generations (anr_hashgrid_force_v1 modes): "default" = forward v1 with
 # backward v2, "v2" = both v2, "v1" = both v1, "v3" = forward v3 (batched gathers) with
 # backward v2, "v4" = forward v4 (one thread per sample) with backward v2
-_HASH_MODES = {"default": 0, "v2": 2, "v1": 1, "v3": 3, "v4": 4}
+_HASH_MODES = {"default": 0, "v2": 2, "v1": 1, "v3": 3, "v4": 4, "v5": 5}
 
 
-@pytest.fixture(params=["default", "v2", "v1", "v3", "v4"])
+@pytest.fixture(params=["default", "v2", "v1", "v3", "v4", "v5"])
 def hash_path(request):
     from atmonr_amd import _lib
 
@@ -790,8 +790,9 @@ def test_ingp_field_bench_size(dev, mma):
 
 @pytest.mark.parametrize("tdt", ["f16", "f32"])
 def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
-    """The per-sample forward (v4) and the walker (v1) evaluate the same corner order and
-    fma chain: identical outputs, f16 and f32 tables, at a bench-like shape."""
+    """The per-sample forward (v4), the compacted-gather walker (v5, f16 tables) and the
+    walker (v1) evaluate the same corner order and fma chain: identical outputs, f16 and
+    f32 tables, at a bench-like shape."""
     from atmonr_amd import _lib
 
     d = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, 19)
@@ -801,7 +802,8 @@ def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
     table = ((torch.rand(d.n_params, device=dev, generator=gen) * 2 - 1) * 1e-2).to(dt)
     outs = []
     lib = _lib.load()
-    for mode in (1, 4):
+    modes = (1, 4, 5) if tdt == "f16" else (1, 4)  # v5: f16 tables
+    for mode in modes:
         prev = lib.anr_hashgrid_force_v1(mode)
         out = torch.empty(x.shape[0], 32, device=dev, dtype=dt)
         _lib.call("anr_hashgrid_fwd", ctypes.byref(d), x.data_ptr(), 3, x.shape[0],
@@ -809,4 +811,5 @@ def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
                   32, _lib.stream(dev))
         lib.anr_hashgrid_force_v1(prev)
         outs.append(out)
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)

@@ -1,0 +1,50 @@
+"""Per-kernel steady-state counter table from tools/sq_bench.sh output.
+
+    python tools/pmc_table.py gpurun_out/sq_bench [kernel-substring ...]
+
+Each counter: median over the second half of the kernel's launches (the bench network
+is alive from step ~7; tools/liveness.py)."""
+
+from __future__ import annotations
+
+import collections
+import csv
+import glob
+import os
+import sys
+
+KERNELS = {"hash_fwd": "hashgrid_fwd_kernel<3, 2, __half, __half>",
+           "hash_bwd": "hashgrid_bwd_v2_kernel<3, float>",
+           "field_fwd": "field::fwd_kernel<64, 2, false, false>",
+           "field_bwd": "field::bwd_kernel<64, 2, true, false, false>",
+           "sampler": "sample_uniform_bins_kernel",
+           "comp_fwd": "rb::fwd_kernel<float, 4, 1, 4>",
+           "comp_bwd": "rb::bwd_kernel<float, 4, 1, 4>"}
+
+
+def main(src):
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(src, "p*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            for tag, pat in KERNELS.items():
+                if pat in r["Kernel_Name"]:
+                    vals[tag][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for tag in KERNELS:
+        if tag not in vals:
+            continue
+        print(f"== {tag}")
+        med = {}
+        for c, v in vals[tag].items():
+            tail = sorted(v[len(v) // 2:])
+            med[c] = tail[len(tail) // 2]
+        for c in sorted(med):
+            print(f"  {c:34s} {med[c]:.4g}")
+        wc = med.get("SQ_WAVE_CYCLES")
+        if wc:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in med:
+                    print(f"  {c + ' / WAVE_CYCLES':34s} {med[c] / wc:.3f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -82,17 +82,41 @@ __device__ __forceinline__ f4 mma32(h8 a, h8 b, f4 c) {
 }
 // dW accumulation: the accumulator lives in AGPRs for the whole kernel (the rest of the
 // kernel's MFMAs write VGPRs). The compiler does not see these as MFMAs, so every VALU
-// access to an accumulator goes through agpr_fence() first (result-latency wait states).
+// access to an accumulator goes through agpr_fence() + agpr_pin() first (result-latency
+// wait states); volatile keeps them in program order with the fence.
 template <bool BF>
 __device__ __forceinline__ void mma32_acc(f4& acc, h8 a, h8 b) {
   if constexpr ((FIELD_EXP & 1) != 0) return;
   if constexpr (BF)
-    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
   else
-    asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// the same with operands fresh from VALU (the register-transposed backward): two wait
+// states between a VALU write of an operand and the MFMA reading it (hipcc pads nothing
+// inside an asm statement). Volatile, so these stay in program order with agpr_fence():
+// the register allocator may copy the accumulators between AGPRs at a loop exit
+// (v_accvgpr_mov / _read, measured in the bf16 W=64 instantiation), and such a copy must
+// not read an accumulator that an MFMA is still writing — every tile ends with a fence.
+template <bool BF>
+__device__ __forceinline__ void mma32_acc_v(f4& acc, h8 a, h8 b) {
+  if constexpr ((FIELD_EXP & 1) != 0) return;
+  if constexpr (BF)
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 __device__ __forceinline__ void agpr_fence() {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+}
+// After agpr_fence(): an empty volatile asm that "rewrites" each accumulator, so no read
+// or copy of it (v_accvgpr_read / _mov are register-only, which a "memory" clobber does
+// not order) can be scheduled above the fence.
+template <int N>
+__device__ __forceinline__ void agpr_pin(f4 (&acc)[N]) {
+  if constexpr ((FIELD_EXP & 1) != 0) return;
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+a"(acc[i]));
 }
 template <bool BF>
 __device__ __forceinline__ f4 mma16(h4 a, h4 b, f4 c) {
@@ -970,6 +994,13 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
       }
     }
     STAMP(6);
+    // see mma32_acc_v: no loop-exit copy of an accumulator while an MFMA still writes it
+    agpr_fence();
+    agpr_pin(dD2);
+    agpr_pin(dD1);
+    agpr_pin(dD0);
+    agpr_pin(dP1);
+    agpr_pin(dP0);
   };
   for (int64_t tile = t_begin; tile < t_full_end; ++tile) process(std::integral_constant<bool, true>{}, tile);
   for (int64_t tile = t_full_end > t_begin ? t_full_end : t_begin; tile < t_end; ++tile)
@@ -982,7 +1013,304 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
   }
 #endif
   agpr_fence();
+  agpr_pin(dD2);
+  agpr_pin(dD1);
+  agpr_pin(dD0);
+  agpr_pin(dP1);
+  agpr_pin(dP0);
   // ---- flush: lane holds dW[n = 16·ntile + 4g + i][k = 16·ktile + li]
+  auto flush = [&](float* dst, int ld, const f4& d, int n0, int k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (d[i] != 0.0f) atomicAdd(dst + (n0 + 4 * g + i) * ld + k, d[i] * inv_s);
+  };
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt) {
+    flush(a.g_dir + N::D2, W, dD2[kt], 0, 16 * kt + li);
+    flush(a.g_pos + N::P1, W, dP1[kt], 0, 16 * kt + li);
+  }
+  if constexpr (NHD == 2) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) flush(a.g_dir + N::D1, W, dD1[nt * NT + kt], 16 * nt, 16 * kt + li);
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      flush(a.g_dir + N::D0, 32, dD0[nt * 2 + kt], 16 * nt, dir_col(16 * kt + li));
+      flush(a.g_pos + N::P0, 32, dP0[nt * 2 + kt], 16 * nt, 16 * kt + li);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Backward v2, register-transposed: the same math and flush as bwd_kernel, but no layer
+// input or gradient tile goes through LDS (LDS holds only the packed weights).
+//
+// dW += G^T · X contracts over the samples, so both operands need the samples along K
+// (lane = unit, samples in the lane's registers) while the chain holds every tile with
+// lane = sample. The transpose is one MFMA against a constant 0/1 matrix: a C-layout
+// tile (lane = sample l&15, units 4g..4g+3) read as the A operand of a 16x16x16 MFMA is
+// the tile with samples as rows, and times the identity it comes back in C layout with
+// lane = unit l&15 and samples 4g..4g+3 — exact (one 1·x product per output, the other
+// terms 0·x = 0 for finite x). Tiles held as 8-slot B operands (the encoding, the dir
+// input) go through a 16x16x32 MFMA against [I|0] or [0|I]. The dW A operand of a
+// 32-sample tile is then cat(transpose(half 0), transpose(half 1)), i.e. samples in the
+// order (4g..4g+3, 16+4g..16+4g+3) along K, and the B operand the same: the contraction
+// is order-blind, and the accumulator layout (and with it the flush) is bwd_kernel's.
+// ReLU masks are the forward's activations, kept in registers.
+// ---------------------------------------------------------------------------------
+template <bool BF>
+struct TrConst {
+  h4 id;      // I16 as a 16x16x16 B operand: lane (column c = l&15) holds rows 4g..4g+3
+  h8 sel[2];  // [I16; 0] and [0; I16] (32 x 16) as 16x16x32 B operands: slot 16kb + c
+  __device__ void init(int lane) {
+    const int c = lane & 15, g = lane >> 4;
+    const _Float16 one = cvt1<BF>(1.0f), zero = cvt1<BF>(0.0f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) id[i] = 4 * g + i == c ? one : zero;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sel[kb][j] = 8 * g + j == 16 * kb + c ? one : zero;
+  }
+};
+// C-layout tile (lane = sample, 4 units) -> (lane = unit, 4 samples)
+template <bool BF>
+__device__ __forceinline__ h4 tr_c(h4 t, h4 id) {
+  return to_h4<BF>(mma16<BF>(t, id, f4{0.0f, 0.0f, 0.0f, 0.0f}));
+}
+// B-operand tile (lane = sample, slots 8g..8g+7) -> (lane = slot 16kb + l&15, 4 samples)
+template <bool BF>
+__device__ __forceinline__ h4 tr_b(h8 x, h8 sel) {
+  return to_h4<BF>(mma32<BF>(x, sel, f4{0.0f, 0.0f, 0.0f, 0.0f}));
+}
+
+template <int W, int NHD, bool FAST, bool ROWS, bool BF>
+__global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64_t tpw,
+                                                     const float* wmax) {
+  using N = Net<W, NHD>;
+  constexpr int NT = N::NT, KB = N::KB;
+  __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
+  for (int e = threadIdx.x * 8; e < N::n_packed; e += blockDim.x * 8)
+    *reinterpret_cast<h8*>(wsm + e) = *reinterpret_cast<const h8*>(a.packed + e);
+  __syncthreads();
+  // per-tile opaque copy of the fragment base: the weight fragments are re-read from LDS
+  // each tile instead of being hoisted into registers
+  const _Float16* wbt = wsm;
+  auto bfrag32 = [&](int off) { return *reinterpret_cast<const h8*>(wbt + off + lane * 8); };
+  auto bfrag16 = [&](int off) { return *reinterpret_cast<const h4*>(wbt + off + lane * 4); };
+  TrConst<BF> tc;
+  tc.init(lane);
+
+  const int64_t n_tiles = (a.M + 31) / 32;
+  const int64_t w_id = static_cast<int64_t>(blockIdx.x) * waves + wave;
+  const int64_t t_begin = w_id * tpw;
+  const int64_t t_end = t_begin + tpw < n_tiles ? t_begin + tpw : n_tiles;
+  const int64_t n_full = a.M / 32;
+
+  f4 dD2[NT], dD1[NHD == 2 ? NT * NT : 1], dD0[NT * 2], dP1[NT], dP0[NT * 2];
+  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < NT; ++i) dD2[i] = dP1[i] = z4;
+#pragma unroll
+  for (int i = 0; i < NT * 2; ++i) dD0[i] = dP0[i] = z4;
+  if constexpr (NHD == 2) {
+#pragma unroll
+    for (int i = 0; i < NT * NT; ++i) dD1[i] = z4;
+  }
+  float s = 1.0f, inv_s = 1.0f;
+  if constexpr (!BF) {
+    const float gm = t_begin < t_end ? wmax[w_id] : 0.0f;
+    if (gm > 0.0f) {
+      int e = static_cast<int>(floorf(log2f(target / gm)));
+      e = e < -60 ? -60 : (e > 100 ? 100 : e);
+      s = ldexpf(1.0f, e);
+      inv_s = ldexpf(1.0f, -e);
+    }
+  }
+
+  Rows cur[2];
+  RawRows nraw[2];
+  const int64_t t_full_end = t_end < n_full ? t_end : n_full;
+  if constexpr (FAST) {
+    if (t_begin < t_full_end) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, t_begin * 32 + mt * 16 + li, g, nraw[mt]);
+    }
+  }
+  auto process = [&](auto full_c, int64_t tile) {
+    constexpr bool FULL = decltype(full_c)::value;
+    {
+      int zoff = 0;
+      asm volatile("" : "+v"(zoff));
+      wbt = wsm + zoff;
+    }
+    if constexpr (FAST && FULL) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) raw_to_rows(nraw[mt], g, cur[mt]);
+      const int64_t tn = tile + 1 < t_full_end ? tile + 1 : tile;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, tn * 32 + mt * 16 + li, g, nraw[mt]);
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) load_rows<ROWS>(a, tile * 32 + mt * 16 + li, g, true, cur[mt]);
+    }
+    const bool full = FULL;
+    // ---- forward recompute of both 16-sample halves; every activation stays in registers
+    Tile<W, NHD> t[2];
+    h4 gc[2];
+    bool dens[2];
+    {
+      bool valid[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) valid[mt] = full || tile * 32 + mt * 16 + li < a.M;
+      FwdWeights<W, NHD> fwl;
+      fwl.load(wbt, lane);
+      tile_forward<W, NHD, 2, BF>(fwl, cur, valid, g, t, NoSink{});
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        dens[mt] = t[mt].po[0] > 0.0f;
+        f4 gv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gv[i] = t[mt].col[i] > 0.0f ? cur[mt].dc[i] * s : 0.0f;
+        gc[mt] = to_h4<BF>(gv);
+      }
+    }
+    auto last = [&](int mt, int kt) -> h4 { return NHD == 2 ? t[mt].hd1[kt] : t[mt].hd0[kt]; };
+    // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
+    h4 dl[2][NT];
+    {
+      const h8 ga = cat(tr_c<BF>(gc[0], tc.id), tr_c<BF>(gc[1], tc.id));
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        const h8 xl = cat(tr_c<BF>(last(0, kt), tc.id), tr_c<BF>(last(1, kt), tc.id));
+        mma32_acc_v<BF>(dD2[kt], ga, xl);
+        const h4 wf = bfrag16(N::oBD2 + kt * N::F16);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) dl[mt][kt] = mask_h4<BF>(mma16<BF>(wf, gc[mt], z4), last(mt, kt));
+      }
+    }
+    // ---- dir hidden layer 1 (NHD == 2): dW_D1 (W x W) += dl^T · X_d0 ; dh0 = D1^T dl
+    h4 dh0[2][NT];
+    if constexpr (NHD == 2) {
+      h8 gb[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) gb[nt] = cat(tr_c<BF>(dl[0][nt], tc.id), tr_c<BF>(dl[1][nt], tc.id));
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        const h8 xb = cat(tr_c<BF>(t[0].hd0[kt], tc.id), tr_c<BF>(t[1].hd0[kt], tc.id));
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) mma32_acc_v<BF>(dD1[nt * NT + kt], gb[nt], xb);
+      }
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        f4 acc[2] = {z4, z4};
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          const h8 wf = bfrag32(N::oBD1 + (kt * KB + kb) * N::F32);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf, cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) dh0[mt][kt] = mask_h4<BF>(acc[mt], t[mt].hd0[kt]);
+      }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int kt = 0; kt < NT; ++kt) dh0[mt][kt] = dl[mt][kt];
+    }
+    // ---- dir input layer: dW_D0 (W x 32, k' order) += dh0^T · X_de ; dpos = D0^T dh0
+    h4 dpo[2];
+    {
+      const h8 x0 = cat(tr_b<BF>(t[0].xd, tc.sel[0]), tr_b<BF>(t[1].xd, tc.sel[0]));
+      const h8 x1 = cat(tr_b<BF>(t[0].xd, tc.sel[1]), tr_b<BF>(t[1].xd, tc.sel[1]));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const h8 gd = cat(tr_c<BF>(dh0[0][nt], tc.id), tr_c<BF>(dh0[1][nt], tc.id));
+        mma32_acc_v<BF>(dD0[nt * 2], gd, x0);
+        mma32_acc_v<BF>(dD0[nt * 2 + 1], gd, x1);
+      }
+      f4 acc[2] = {z4, z4};
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const h8 wf = bfrag32(N::oBD0 + kb * N::F32);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf, cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        // pos_out[:, 0] is the density: its gradient is dL/dsigma through the ReLU
+        const float dsv = dens[mt] ? cur[mt].ds * s : 0.0f;
+        acc[mt][0] = g == 0 ? dsv : acc[mt][0];
+        dpo[mt] = to_h4<BF>(acc[mt]);
+      }
+    }
+    // ---- pos output layer: dW_P1 (16 x W) += dpo^T · X_ph ; dhp = P1^T dpo
+    h4 dhp[2][NT];
+    {
+      const h8 ga = cat(tr_c<BF>(dpo[0], tc.id), tr_c<BF>(dpo[1], tc.id));
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        const h8 xp = cat(tr_c<BF>(t[0].hp[kt], tc.id), tr_c<BF>(t[1].hp[kt], tc.id));
+        mma32_acc_v<BF>(dP1[kt], ga, xp);
+        const h4 wf = bfrag16(N::oBP1 + kt * N::F16);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) dhp[mt][kt] = mask_h4<BF>(mma16<BF>(wf, dpo[mt], z4), t[mt].hp[kt]);
+      }
+    }
+    // ---- pos input layer: dW_P0 (W x 32) += dhp^T · X_pe ; d_enc = P0^T dhp
+    {
+      const h8 x0 = cat(tr_b<BF>(t[0].xe, tc.sel[0]), tr_b<BF>(t[1].xe, tc.sel[0]));
+      const h8 x1 = cat(tr_b<BF>(t[0].xe, tc.sel[1]), tr_b<BF>(t[1].xe, tc.sel[1]));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const h8 gp = cat(tr_c<BF>(dhp[0][nt], tc.id), tr_c<BF>(dhp[1][nt], tc.id));
+        mma32_acc_v<BF>(dP0[nt * 2], gp, x0);
+        mma32_acc_v<BF>(dP0[nt * 2 + 1], gp, x1);
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f4 acc[2] = {z4, z4};
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          const h8 wf = bfrag32(N::oBP0 + (kt * KB + kb) * N::F32);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf, cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int64_t row = tile * 32 + mt * 16 + li;
+          if (full || row < a.M) {
+            const f4 v = acc[mt] * inv_s;
+            *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
+          }
+        }
+      }
+    }
+    // the last dW MFMAs of the tile have written their accumulators before anything
+    // (a loop-exit copy) reads them
+    agpr_fence();
+    agpr_pin(dD2);
+    agpr_pin(dD1);
+    agpr_pin(dD0);
+    agpr_pin(dP1);
+    agpr_pin(dP0);
+  };
+  for (int64_t tile = t_begin; tile < t_full_end; ++tile) process(std::integral_constant<bool, true>{}, tile);
+  for (int64_t tile = t_full_end > t_begin ? t_full_end : t_begin; tile < t_end; ++tile)
+    process(std::integral_constant<bool, false>{}, tile);
+
+  agpr_fence();
+  agpr_pin(dD2);
+  agpr_pin(dD1);
+  agpr_pin(dD0);
+  agpr_pin(dP1);
+  agpr_pin(dP0);
   auto flush = [&](float* dst, int ld, const f4& d, int n0, int k) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1012,6 +1340,9 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 // host side
 // ---------------------------------------------------------------------------------
 static int g_target_log2 = 6;  // f16 gradient scale: max |dL/dout| of a wavefront -> 2^6
+// backward kernel generation: 0 = LDS tiles (bwd_kernel), 1 = register-transposed
+// (bwd_rt_kernel); test / A-B hook anr_ingp_field_force_bwd
+static int g_bwd_mode = 1;
 
 // Backward launch geometry: one resident wavefront per slot (4 per block), each owning a
 // contiguous range of 32-sample tiles. The f16 backward needs one float per wavefront of
@@ -1020,15 +1351,21 @@ struct BwdGeom {
   int64_t blocks, nw, tpw;
 };
 template <int W, int NHD, bool BF>
-static BwdGeom bwd_geom(int64_t M, bool fast) {
+static const void* bwd_fn(bool fast, int mode) {
+  if (mode == 1)
+    return fast ? reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, true, false, BF>)
+                : reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, false, false, BF>);
+  return fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true, false, BF>)
+              : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false, false, BF>);
+}
+template <int W, int NHD, bool BF>
+static BwdGeom bwd_geom(int64_t M, bool fast, int mode) {
   const int waves = 4;
-  const void* fn = fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true, false, BF>)
-                        : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false, false, BF>);
-  static int pc[2] = {0, 0};
-  int& p = pc[fast ? 1 : 0];
+  static int pc[2][2] = {{0, 0}, {0, 0}};
+  int& p = pc[mode][fast ? 1 : 0];
   if (p == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, bwd_fn<W, NHD, BF>(fast, mode), 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
     p = nb;
   }
   const int64_t tiles = (M + 31) / 32;
@@ -1042,9 +1379,15 @@ static BwdGeom bwd_geom(int64_t M, bool fast) {
 template <int W, int NHD, bool BF>
 static int64_t bwd_workspace(int64_t M) {
   if (BF || M <= 0) return 0;
-  // the larger of the two kernels' wave counts (fast and general d_color layouts)
-  const int64_t a = bwd_geom<W, NHD, BF>(M, true).nw, b = bwd_geom<W, NHD, BF>(M, false).nw;
-  return static_cast<int64_t>(sizeof(float)) * (a > b ? a : b);
+  // the largest wave count of the backward kernels (both generations, fast and general
+  // d_color layouts), so a workspace sized once serves whichever runs
+  int64_t n = 0;
+  for (int mode = 0; mode < 2; ++mode)
+    for (int f = 0; f < 2; ++f) {
+      const int64_t w = bwd_geom<W, NHD, BF>(M, f == 1, mode).nw;
+      n = w > n ? w : n;
+    }
+  return static_cast<int64_t>(sizeof(float)) * n;
 }
 
 template <int W, int NHD, bool BF>
@@ -1070,25 +1413,35 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
     return 0;
   }
   const bool fast = a.n_out == 4 && (a.d_color_stride & 3) == 0 && a.d_sigma != nullptr;
-  const size_t lds = (static_cast<size_t>(N::n_packed) + waves * N::wave_lds) * 2;  // static
+  const int mode = g_bwd_mode;
+  const size_t lds = (static_cast<size_t>(N::n_packed) + (mode == 1 ? 0 : waves * N::wave_lds)) * 2;
   if (lds > 160 * 1024) return 1;
-  const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast);
+  const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast, mode);
   if (!BF && (ws == nullptr || ws_bytes < static_cast<int64_t>(sizeof(float)) * gm.nw)) return 2;
   const float target = ldexpf(1.0f, g_target_log2);
   const dim3 grid(static_cast<unsigned>(gm.blocks)), block(64 * waves);
-  if (a.rows) {
-    if (!BF) hipLaunchKernelGGL(absmax_kernel<true>, dim3(gm.nw), dim3(1024), 0, st, a, gm.tpw * 32, ws);
-    if (fast)
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, true, BF>), grid, block, 0, st, a, target, gm.tpw, ws);
+  if (!BF) {
+    if (a.rows)
+      hipLaunchKernelGGL(absmax_kernel<true>, dim3(gm.nw), dim3(1024), 0, st, a, gm.tpw * 32, ws);
     else
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, true, BF>), grid, block, 0, st, a, target, gm.tpw, ws);
-  } else {
-    if (!BF) hipLaunchKernelGGL(absmax_kernel<false>, dim3(gm.nw), dim3(1024), 0, st, a, gm.tpw * 32, ws);
-    if (fast)
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, true, false, BF>), grid, block, 0, st, a, target, gm.tpw, ws);
-    else
-      hipLaunchKernelGGL((bwd_kernel<W, NHD, false, false, BF>), grid, block, 0, st, a, target, gm.tpw, ws);
+      hipLaunchKernelGGL(absmax_kernel<false>, dim3(gm.nw), dim3(1024), 0, st, a, gm.tpw * 32, ws);
   }
+#define ANR_BWD_LAUNCH(K, FASTV, ROWSV) \
+  hipLaunchKernelGGL((K<W, NHD, FASTV, ROWSV, BF>), grid, block, 0, st, a, target, gm.tpw, ws)
+  if (mode == 1) {
+    if (a.rows) {
+      if (fast) ANR_BWD_LAUNCH(bwd_rt_kernel, true, true); else ANR_BWD_LAUNCH(bwd_rt_kernel, false, true);
+    } else {
+      if (fast) ANR_BWD_LAUNCH(bwd_rt_kernel, true, false); else ANR_BWD_LAUNCH(bwd_rt_kernel, false, false);
+    }
+  } else {
+    if (a.rows) {
+      if (fast) ANR_BWD_LAUNCH(bwd_kernel, true, true); else ANR_BWD_LAUNCH(bwd_kernel, false, true);
+    } else {
+      if (fast) ANR_BWD_LAUNCH(bwd_kernel, true, false); else ANR_BWD_LAUNCH(bwd_kernel, false, false);
+    }
+  }
+#undef ANR_BWD_LAUNCH
   return 0;
 }
 
@@ -1163,6 +1516,12 @@ extern "C" int64_t anr_ingp_field_bwd_workspace_bytes(const anr_mlp_desc* pos,
     case 642: return bwd_workspace<64, 2, false>(M);
   }
   return 0;
+}
+
+extern "C" int anr_ingp_field_force_bwd(int32_t mode) {
+  const int prev = g_bwd_mode;
+  if (mode == 0 || mode == 1) g_bwd_mode = mode;
+  return prev;
 }
 
 extern "C" int anr_ingp_field_set_grad_scale(int32_t log2_target) {

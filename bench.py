@@ -289,6 +289,9 @@ def main():
                     help="zero the gradient bucket with a fill instead of in the AdamW pass")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one all-reduce of the whole gradient bucket after backward")
+    ap.add_argument("--field-bwd", choices=["rt", "lds"], default="rt",
+                    help="fused field backward generation (anr_ingp_field_force_bwd): "
+                         "register-transposed (default) or LDS-staged tiles")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every kernel timed (per-kernel breakdown)")
     args = ap.parse_args()
@@ -322,6 +325,7 @@ def main():
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
     from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
 
+    _lib.load().anr_ingp_field_force_bwd(1 if args.field_bwd == "rt" else 0)
     t0 = time.time()
     ds = SyntheticHARP2Dataset(n_views=args.views, img_size=args.img_size, device=dev, seed=0)
     torch.cuda.synchronize()

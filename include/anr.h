@@ -265,6 +265,11 @@ int64_t anr_ingp_field_packed_size(const anr_mlp_desc* pos, const anr_mlp_desc* 
 /* f16 gradient scale target of the backward (max |dL/dout| per wavefront -> 2^v);
  * returns the previous value. Test hook; process-wide. */
 int anr_ingp_field_set_grad_scale(int32_t log2_target);
+/* Backward kernel generation: 0 = layer inputs and gradient tiles staged in LDS, 1 =
+ * register-transposed (default; transposes by MFMA against a 0/1 matrix, LDS holds only
+ * the weights). Same math and results. Test / A-B hook; process-wide; other values keep
+ * the current mode. Returns the previous mode. */
+int anr_ingp_field_force_bwd(int32_t mode);
 int64_t anr_ingp_field_bwd_workspace_bytes(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
                                            int32_t mma_dtype, int64_t M);
 int anr_ingp_field_pack(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,

@@ -29,6 +29,12 @@ static int g_composite_generic = 0;
 
 template <typename T>
 __device__ __forceinline__ float ldv(const T* p, int64_t i) { return to_f32<T>(p[i]); }
+// alpha = 1 - exp(-x) (graphics_utils.py:38) as -expm1(-x): accurate to an ulp of alpha
+// itself. Evaluated as 1 - expf(-x), f32 loses log2(1/x) bits to cancellation, and at
+// BASELINE configs[2]'s 1,024 samples per ray x = sigma * delta is ~1e-6 at
+// initialisation: dL/dcolor = w * dL/dC then carries 2e-2 relative error and the GPU
+// exp's rounding bias accumulates in the dir-MLP gradient (tools/composite_diag.py).
+__device__ __forceinline__ float alpha_of(float x) { return -expm1f(-x); }
 
 // Exclusive multiplicative scan across the wave (lane 0 gets 1).
 __device__ __forceinline__ float wave_excl_prod(float v, int lane) {
@@ -119,7 +125,7 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(CompArgs a) {
 #pragma unroll
     for (int s = 0; s < kMaxCh; ++s) {
       if (s < S) {
-        const float al = 1.0f - expf(-ldv(sig, i * S + s) * dl);
+        const float al = alpha_of(ldv(sig, i * S + s) * dl);
         pt[s] *= (1.0f - al) + 1e-10f;
         pom[s] *= 1.0f - al;
       }
@@ -143,7 +149,7 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(CompArgs a) {
 #pragma unroll
     for (int s = 0; s < kMaxCh; ++s) {
       if (s < S) {
-        const float al = 1.0f - expf(-ldv(sig, i * S + s) * dl);
+        const float al = alpha_of(ldv(sig, i * S + s) * dl);
         w[s] = al * T_in[s];
         T_in[s] *= (1.0f - al) + 1e-10f;
         const int64_t o = (b * N + i) * S + s;
@@ -222,7 +228,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompArgs a) {
       for (int s = 0; s < kMaxCh; ++s)
         if (s < S) {
           if (a.d_weights) q[s] += ldv(static_cast<const T*>(a.d_weights), (bb * N + i) * S + s);
-          const float al = 1.0f - expf(-ldv(sig, i * S + s) * dl);
+          const float al = alpha_of(ldv(sig, i * S + s) * dl);
           const float t = (1.0f - al) + 1e-10f;
           Tloc[i * S + s] = pt[s];
           Ploc[i * S + s] = pom[s];
@@ -268,8 +274,8 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompArgs a) {
           const int64_t o = (bb * N + i) * S + s;
           if (a.d_weights) q[s] += ldv(static_cast<const T*>(a.d_weights), o);
           const float sg = ldv(sig, i * S + s);
-          const float e = expf(-sg * dl);
-          const float al = 1.0f - e;
+          const float al = alpha_of(sg * dl);
+          const float e = 1.0f - al;
           const float t = (1.0f - al) + 1e-10f;
           const float Ti = T_in[s] * Tloc[i * S + s];
           const float Pi = P_in[s] * Ploc[i * S + s];
@@ -425,7 +431,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(CompArgs a) {
   for (int j = 0; j < SPL; ++j)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const float x = 1.0f - expf(-sg[j * S + s] * dl[j]);
+      const float x = alpha_of(sg[j * S + s] * dl[j]);
       al[j * S + s] = j < nvalid ? x : 0.0f;
       pt[s] *= (1.0f - al[j * S + s]) + (j < nvalid ? 1e-10f : 0.0f);
       pom[s] *= 1.0f - al[j * S + s];
@@ -559,9 +565,10 @@ __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
     for (int s = 0; s < S; ++s) {
       const int o = j * S + s;
       if (a.d_weights && j < nvalid) qq[s] += ldv(static_cast<const T*>(a.d_weights), (b * N + i0 + j) * S + s);
-      const float ee = expf(-sg[o] * dl[j]);
+      const float ao = alpha_of(sg[o] * dl[j]);
+      const float ee = 1.0f - ao;
       e[o] = ee;
-      al[o] = j < nvalid ? 1.0f - ee : 0.0f;
+      al[o] = j < nvalid ? ao : 0.0f;
       q[o] = j < nvalid ? qq[s] : 0.0f;
       const float t = (1.0f - al[o]) + (j < nvalid ? 1e-10f : 0.0f);
       Tl[o] = pt[s];

@@ -113,7 +113,8 @@ class RefInstantNGP:
     """Parameters (float64 leaf tensors, flat per module like tcnn) + forward / loss."""
 
     def __init__(self, config: dict, state: dict, prep: dict, scale: float, max_i: float,
-                 half: bool = False, mlp_half=None, semantics: str = "build"):
+                 half: bool = False, mlp_half=None, semantics: str = "build",
+                 composite: str = "f32"):
         self.cfg = config
         self.ingp = config["instant_ngp"]
         self.N = int(config["num_samples_per_ray"])
@@ -127,6 +128,9 @@ class RefInstantNGP:
         if semantics not in ("build", "reference") or (semantics == "reference" and half is not True):
             raise ValueError("semantics='reference' is the reference's f16 path (half=True)")
         self.semantics = semantics
+        # "f32": the composite in f32 as the reference evaluates it; "f64": exact, to
+        # measure how sensitive a gradient is to the composite's f32 rounding
+        self.composite = composite
         self.params = {m: state[m]["params"].detach().cpu().double().clone().requires_grad_(True)
                        for m in MODULES}
         self.pos_grid = _grid_cfg(self.ingp["encoding"], 3)
@@ -170,9 +174,10 @@ class RefInstantNGP:
         # the composite in f32, as the reference evaluates graphics_utils.py in the network
         # output dtype (alpha = 1 - exp(-sigma * delta) cancels in that precision; the
         # GPU composite computes in f32 for every storage dtype)
+        ct = torch.float64 if self.composite == "f64" else torch.float32
         cm, alpha, weights, atmo, surf = ref_path.render_with_surface(
-            z * (self.scale / 1000), color.view(B, N, -1).float(),
-            sigma.view(B, N, 1).float(), color_surf.float())
+            (z * (self.scale / 1000)).to(ct if ct == torch.float64 else z.dtype),
+            color.view(B, N, -1).to(ct), sigma.view(B, N, 1).to(ct), color_surf.to(ct))
         return {"color_map_fine": cm.double(), "color_map_atmo": atmo.double(),
                 "color_map_surf": surf.double(), "weights_fine": weights, "z_vals_fine": z,
                 "color_fine": color.view(B, N, -1)[:, :-1],

@@ -135,11 +135,13 @@ def _grid_inputs(dev, cfg, M, coherent, seed=0):
 
 # hash-grid kernel generations (anr_hashgrid_force_v1 modes): "default" = forward v1 with
 # backward v2, "v2" = both v2, "v1" = both v1, "v3" = forward v3 (batched gathers) with
-# backward v2, "v4" = forward v4 (one thread per sample) with backward v2
-_HASH_MODES = {"default": 0, "v2": 2, "v1": 1, "v3": 3, "v4": 4, "v5": 5}
+# backward v2, "v4" = forward v4 (one thread per sample) with backward v2, "v5" = forward v5
+# (compacted gathers), "v6" = forward v6 (branch-free corners, buffer addressing), "v8" =
+# forward v6 with backward v3 (64-B segment flushes through LDS; forced at every chunk length)
+_HASH_MODES = {"default": 0, "v2": 2, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v6": 6, "v8": 8}
 
 
-@pytest.fixture(params=["default", "v2", "v1", "v3", "v4", "v5"])
+@pytest.fixture(params=["default", "v2", "v1", "v3", "v4", "v5", "v6", "v8"])
 def hash_path(request):
     from atmonr_amd import _lib
 
@@ -179,7 +181,8 @@ def test_hashgrid_fwd_bwd_f32(dev, hash_path, cfg, M, coherent):
     close(dtab, gref, rel=1e-5, atol=1e-5)
 
 
-def test_hashgrid_bench_size_adjoint_and_spot_rows(dev):
+@pytest.mark.parametrize("mode", [0, 8])
+def test_hashgrid_bench_size_adjoint_and_spot_rows(dev, mode):
     """Bench size (8192 rays x 1024 samples, the config-3 grid): the chunk lengths chosen
     only at this size (forward 128, backward 256 samples per chunk) against the oracle on
     4096 spot rows (forward), and the adjoint identity <g, fwd(t)> = <bwd(g), t> over all
@@ -199,6 +202,8 @@ def test_hashgrid_bench_size_adjoint_and_spot_rows(dev):
     table = torch.rand(d.n_params, device=dev, generator=gen) * 2 - 1
     out = torch.empty(M, 32, device=dev)
     s = _lib.stream(dev)
+    lib = _lib.load()
+    prev = lib.anr_hashgrid_force_v1(mode)
     _lib.call("anr_hashgrid_fwd", ctypes.byref(d), x.data_ptr(), 3, M, table.data_ptr(),
               _lib.F32, out.data_ptr(), _lib.F32, out.stride(0), s)
     rows = torch.randint(0, M, (4096,), device=dev, generator=gen)
@@ -208,6 +213,7 @@ def test_hashgrid_bench_size_adjoint_and_spot_rows(dev):
     dtab = torch.zeros(d.n_params, device=dev)
     _lib.call("anr_hashgrid_bwd", ctypes.byref(d), x.data_ptr(), 3, M, g.data_ptr(), _lib.F32,
               g.stride(0), dtab.data_ptr(), s)
+    lib.anr_hashgrid_force_v1(prev)
     lhs = torch.dot(g.flatten().double(), out.flatten().double()).item()
     rhs = torch.dot(dtab.double(), table.double()).item()
     scale = torch.dot(g.flatten().double().abs(), out.flatten().double().abs()).item()
@@ -850,9 +856,9 @@ def test_ingp_field_bench_size(dev, mma):
 
 @pytest.mark.parametrize("tdt", ["f16", "f32"])
 def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
-    """The per-sample forward (v4), the compacted-gather walker (v5, f16 tables) and the
-    walker (v1) evaluate the same corner order and fma chain: identical outputs, f16 and
-    f32 tables, at a bench-like shape."""
+    """The per-sample forward (v4), the compacted-gather walker (v5, f16 tables), the
+    buffer-addressed walker (v6) and the walker (v1) evaluate the same corner order and fma
+    chain: identical outputs, f16 and f32 tables, at a bench-like shape."""
     from atmonr_amd import _lib
 
     d = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, 19)
@@ -862,7 +868,7 @@ def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
     table = ((torch.rand(d.n_params, device=dev, generator=gen) * 2 - 1) * 1e-2).to(dt)
     outs = []
     lib = _lib.load()
-    modes = (1, 4, 5) if tdt == "f16" else (1, 4)  # v5: f16 tables
+    modes = (1, 4, 5, 6) if tdt == "f16" else (1, 4, 6)  # v5: f16 tables
     for mode in modes:
         prev = lib.anr_hashgrid_force_v1(mode)
         out = torch.empty(x.shape[0], 32, device=dev, dtype=dt)
@@ -873,3 +879,42 @@ def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
         outs.append(out)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
+
+
+@pytest.mark.parametrize("cfg,M,xs", [((3, 16, 16, 1.3819, 19), 100003, 3),
+                                      ((3, 6, 4, 2.0, 10), 5001, 4),
+                                      ((2, 16, 16, 1.3819, 19), 70001, 5),
+                                      ((3, 16, 16, 1.3819, 19), 1, 3)])
+@pytest.mark.parametrize("tdt", ["f16", "f32"])
+def test_hashgrid_fwd_v6_outside_grid_and_strides(dev, cfg, M, xs, tdt):
+    """v6 against v1, bit for bit, where v6's shortcuts matter: coordinates outside [0, 1]
+    (dense levels wrap modulo T; the far-face test must send them down the exact path),
+    coordinate and output row strides wider than the data, a ragged final chunk and a
+    single sample (loads past the end of x return 0, stores past the last row drop)."""
+    from atmonr_amd import _lib
+
+    D, L = cfg[0], cfg[1]
+    d = _lib.hashgrid_desc(D, L, 2, cfg[2], cfg[3], cfg[4])
+    gen = torch.Generator(device=dev).manual_seed(11)
+    R = -(-M // 97)
+    o = torch.rand(R, 1, D, device=dev, generator=gen) * 2.0 - 0.5
+    dr = (torch.rand(R, 1, D, device=dev, generator=gen) - 0.5) * 0.4
+    t = torch.linspace(0, 1, 97, device=dev)[None, :, None]
+    xx = (o + dr * t).reshape(-1, D)[:M]
+    x = torch.zeros(M, xs, device=dev)
+    x[:, :D] = xx
+    x[::7, :D] = x[::7, :D].clamp(0, 1)  # exact faces too
+    dt = torch.float16 if tdt == "f16" else torch.float32
+    table = ((torch.rand(d.n_params, device=dev, generator=gen) * 2 - 1) * 1e-2).to(dt)
+    lib = _lib.load()
+    outs = []
+    for mode in (1, 6):
+        prev = lib.anr_hashgrid_force_v1(mode)
+        out = torch.full((M + 1, L * 2 + 3), -9.0, device=dev, dtype=dt)
+        _lib.call("anr_hashgrid_fwd", ctypes.byref(d), x.data_ptr(), xs, M, table.data_ptr(),
+                  _lib.dtype_code(dt), out.data_ptr(), _lib.dtype_code(dt), L * 2 + 3,
+                  _lib.stream(dev))
+        lib.anr_hashgrid_force_v1(prev)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    assert torch.all(outs[1][:, L * 2:] == -9) and torch.all(outs[1][M] == -9)

@@ -1,0 +1,76 @@
+"""A/B of the hash-grid forward generations at bench size (profiling aid).
+
+    python tools/hash_fwd_ab.py [--modes 0,6,7] [--iters 10] [--log2t 19]
+
+Bench coordinates (synthetic HARP2 scene -> fused sampler, 8192 rays x 1024 samples), f16
+table, f16 output. Mode 7 writes level-major planes [L][M][2]; its output is compared bit
+for bit with mode 1's row-major output. Prints the HIP-event average per mode.
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "atmospheric-neural-rendering_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from atmonr_amd import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rays", type=int, default=8192)
+    ap.add_argument("--samples", type=int, default=1024)
+    ap.add_argument("--log2t", type=int, default=19)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--modes", default="1,6,7")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    B, N = args.rays, args.samples
+    M = B * N
+    from atmonr_amd.batch_loader import BatchLoader
+    from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
+    from atmonr_amd.samplers import sample_and_preprocess
+
+    ds = SyntheticHARP2Dataset(n_views=8, img_size=512, device=dev, seed=0)
+    batch = next(iter(BatchLoader(ds, B, shuffle=True, seed=0)))
+    prep = ds.get_point_preprocessor("horizontal").params(ngp_remap=True, alt_compress=8.0)
+    _, _, coords = sample_and_preprocess(batch, N, prep)
+    x = coords.reshape(M, 3).contiguous()
+    desc = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, args.log2t)
+    table = ((torch.rand(desc.n_params, device=dev) * 2 - 1) * 1e-2).half()
+    lib = _lib.load()
+    s = _lib.stream(dev)
+    outs = {}
+    for mode in [int(m) for m in args.modes.split(",")]:
+        planar = mode == 7
+        enc = torch.empty((16, M, 2) if planar else (M, 32), device=dev, dtype=torch.float16)
+        prev = lib.anr_hashgrid_force_v1(mode)
+        timer = _lib.KernelTimer()
+        for it in range(args.iters + 2):
+            if it == 2:
+                timer.__enter__()
+            _lib.call("anr_hashgrid_fwd", ctypes.byref(desc), x.data_ptr(), 3, M,
+                      table.data_ptr(), _lib.F16, enc.data_ptr(), _lib.F16, 32, s,
+                      tag=f"hash_fwd_m{mode}")
+        timer.__exit__(None, None, None)
+        torch.cuda.synchronize()
+        lib.anr_hashgrid_force_v1(prev)
+        for k, v in timer.summary().items():
+            print(f"mode {mode}: {k} avg {v['avg_ms']:.4f} ms ({v['launches']} calls)", flush=True)
+        outs[mode] = enc.permute(1, 0, 2).reshape(M, 32) if planar else enc
+    ref = outs.get(1)
+    if ref is not None:
+        for m, o in outs.items():
+            print(f"mode {m} equal to mode 1: {torch.equal(o, ref)}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

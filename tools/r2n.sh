@@ -1,0 +1,10 @@
+set -o pipefail
+# hash backward v3 (mode 8): parity then bench A/B against the default
+O=gpurun_out/r2n; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -x -v -m gpu -k "hashgrid" --timeout 300 --timeout-method thread > $O/pytest_hash.log 2>&1 || exit $?
+for m in 0 8 0 8; do
+  ANR_HASHGRID_MODE=$m timeout -k 10 200 python -u bench.py --no-cpu-baseline --spec-peaks > $O/bench_mode$m.log 2>&1 || exit $?
+  grep -h metric $O/bench_mode$m.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('mode $m', d['value'], d['ms_per_step'], d['final_loss'], {k: v['avg_ms'] for k, v in d['kernels'].items() if k.startswith('hash')})" >> $O/summary.txt
+done
+echo done

@@ -26,9 +26,6 @@
 #ifndef HASH_BS
 #define HASH_BS 8  // samples per prefetch batch of the v2 backward walker
 #endif
-#ifndef HASH_BS3
-#define HASH_BS3 4  // samples per prefetch batch of the v3 backward walker (vector loads)
-#endif
 #ifndef HASH_FBS
 #define HASH_FBS 4  // samples per coordinate prefetch batch of the forward walker
 #endif
@@ -943,7 +940,8 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v5_kernel(
 //     the walk has no per-sample bounds checks and a wave-uniform trip count;
 //   * f16 corner features are interpolated straight from the packed pair (v_fma_mix_f32
 //     reads the f16 operand in place: no conversions).
-// Same corner order, weights and fma chain as v1: results are bit-identical to it.
+// Same corner order, weights and fma chain as v1: results are bit-identical to it. The
+// default forward since r02 (0.667 -> 0.648 ms at bench size).
 template <typename TT>
 struct Raw2;
 template <>
@@ -1128,148 +1126,6 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v6_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Forward v7 (F = 2, L <= 16, level-major output planes out[l][m][f]): one LEVEL per
-// workgroup, 256 chunks per workgroup (one per lane), levels placed on XCDs. Workgroups
-// are dispatched to the 8 XCDs round-robin, so slot s = blockIdx % 16 runs on XCD s % 8;
-// slot s < 8 serves level s and slot s >= 8 level 23 - s: XCD k holds levels {k, 15 - k},
-// at most one 2 MiB hashed fine level next to a dense coarse one (or two little-used middle
-// levels), so a level's corner gathers are served from its XCD's 4 MiB L2 instead of the
-// die-level cache. The level is wave-uniform: the hashed / dense choice is a scalar branch,
-// and a coarse level's wavefront takes the gather path only when one of its 64 chunks
-// enters a new cell. Results bit-identical to v1 (same corners, weights and fma chain).
-template <int D, typename TT, typename TO>
-__global__ void __launch_bounds__(256) hashgrid_fwd_v7_kernel(
-    GridLevels G, int n_levels, const float* __restrict__ x, uint32_t x_bytes, uint32_t xs4,
-    int64_t M, int K, const TT* __restrict__ table, uint32_t table_bytes,
-    TO* __restrict__ out, uint32_t out_bytes, uint32_t plane_bytes) {
-  using R = Raw2<TT>;
-  const int slot = static_cast<int>(blockIdx.x & 15);
-  const int level = slot < 8 ? slot : 23 - slot;
-  if (level >= n_levels) return;  // block-uniform
-  const int64_t chunk = static_cast<int64_t>(blockIdx.x >> 4) * blockDim.x + threadIdx.x;
-  const int64_t m0 = chunk * K;
-  if (m0 >= M) return;
-  const __amdgpu_buffer_rsrc_t rx = wave_rsrc(x, x_bytes);
-  const __amdgpu_buffer_rsrc_t rt = wave_rsrc(table, table_bytes);
-  const __amdgpu_buffer_rsrc_t ro = wave_rsrc(out, out_bytes);
-
-  const float scale = G.scale[level];
-  const uint32_t res = G.res[level];
-  const uint32_t T = G.size[level];
-  const uint32_t base = G.offset[level] * R::bytes;
-  LevelIdx<D> li;
-  li.init(T, res);
-  const uint32_t hmask = T - 1u;
-
-  // rows past M would land in the next plane: their stores get an out-of-range offset
-  const int64_t rem64 = M - m0;
-  const int rem = rem64 < K ? static_cast<int>(rem64) : K;
-  uint32_t xo = static_cast<uint32_t>(m0) * xs4;
-  uint32_t oo = static_cast<uint32_t>(level) * plane_bytes +
-                static_cast<uint32_t>(m0) * 2u * static_cast<uint32_t>(sizeof(TO));
-
-  uint32_t cell[D];
-  bool have = false;
-#pragma unroll
-  for (int d = 0; d < D; ++d) cell[d] = 0u;
-  typename R::type val[1 << D];
-#pragma unroll
-  for (int c = 0; c < (1 << D); ++c) val[c] = {};
-
-  auto step = [&](const float* xv, int j) {
-    float w[D];
-    uint32_t g[D];
-    bool same = have;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const float p = fmaf(scale, xv[d], 0.5f);
-      const float fl = floorf(p);
-      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
-      w[d] = p - fl;
-      same = same && (g[d] == cell[d]);
-    }
-    if (!same) {
-      uint32_t comp[D][2];
-      li.dims(g, comp);
-      uint32_t idx[1 << D];
-      if (li.hashed) {  // wave-uniform
-#pragma unroll
-        for (int c = 0; c < (1 << D); ++c) {
-          uint32_t hx = 0u;
-#pragma unroll
-          for (int d = 0; d < D; ++d) hx ^= comp[d][(c >> d) & 1];
-          idx[c] = hx & hmask;
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < (1 << D); ++c) {
-          uint32_t sm = 0u;
-#pragma unroll
-          for (int d = 0; d < D; ++d) sm += comp[d][(c >> d) & 1];
-          idx[c] = sm;
-        }
-        uint32_t gmax = g[0];
-#pragma unroll
-        for (int d = 1; d < D; ++d) gmax = gmax > g[d] ? gmax : g[d];
-        if (gmax >= res - 1u) {
-#pragma unroll
-          for (int c = 0; c < (1 << D); ++c)
-            if (idx[c] >= T) {
-              const uint32_t s1 = idx[c] - T;
-              idx[c] = s1 < T ? s1 : idx[c] % T;
-            }
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, base + idx[c] * R::bytes);
-#pragma unroll
-      for (int d = 0; d < D; ++d) cell[d] = g[d];
-      have = true;
-    }
-    float a0 = 0.0f, a1 = 0.0f;
-#pragma unroll
-    for (int c = 0; c < (1 << D); ++c) {
-      float wt = 1.0f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
-      R::fma2(wt, val[c], a0, a1);
-    }
-    store2<TO>(ro, j < rem ? oo : 0xffffffffu, a0, a1);
-    oo += 2u * static_cast<uint32_t>(sizeof(TO));
-  };
-
-  constexpr int BS = HASH_FBS;
-  float xb[BS][D], xn[BS][D];
-  auto load_batch = [&](float (*xo_)[D]) {
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      if constexpr (D == 3) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rx, xo, 0, 0);
-        xo_[j][0] = __uint_as_float(v[0]);
-        xo_[j][1] = __uint_as_float(v[1]);
-        xo_[j][2] = __uint_as_float(v[2]);
-      } else {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rx, xo, 0, 0);
-        xo_[j][0] = __uint_as_float(v[0]);
-        xo_[j][1] = __uint_as_float(v[1]);
-      }
-      xo += xs4;
-    }
-  };
-  load_batch(xb);
-  for (int jb = 0; jb < K; jb += BS) {
-    load_batch(xn);
-#pragma unroll
-    for (int j = 0; j < BS; ++j)
-      if (jb + j < K) step(xb[j], jb + j);
-#pragma unroll
-    for (int j = 0; j < BS; ++j)
-#pragma unroll
-      for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
-  }
-}
-
 template <int D, typename TG>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
@@ -1379,282 +1235,6 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Backward v3 (F = 2, L <= 16, long chunks): v2's walker (4 lanes per level, one chunk per
-// wavefront, the cell's corner gradients accumulated in registers) with the gradients
-// flushed per 64-B SEGMENT instead of per corner pair. The kernel is bound by the rate of
-// memory-side atomic requests (one per 64-B segment a wave instruction touches), and v2's
-// requests carry 16 B: a level's (x, x + 1) pair of one yz row. Here a wavefront keeps, in
-// LDS, the 8-entry x-block segments of every yz row its current cell touches (8 entries x 2
-// f32 features = 64 B, exactly one request; on hashed levels the block x = 8B..8B+7 of a
-// row maps to ONE aligned 8-entry block of the table, permuted by the hash's low bits,
-// because the first hash prime is 1). On a cell change the lanes add their corner sums
-// into the segments (ds_add_f32) and queue the segments the new cell no longer touches;
-// the whole wavefront then flushes the queue, 16 lanes (8 entries x 2 features) per
-// segment, one global atomic instruction per 4 segments. Moves inside an x-block flush
-// nothing. Simulated on bench-like rays: 3.23 -> 2.14 requests per sample.
-// Segments live in parity slots (x-block & 1, y & 1, z & 1): the segments of one cell
-// never share a slot, and a slot is flushed and zeroed before the cell that reuses it adds.
-template <int D>
-struct SegLayout {
-  static constexpr int NR = 1 << (D - 1);  // yz rows of a cell
-  static constexpr int NS = 2 * NR;        // parity slots per level (x-block parity x rows)
-  static constexpr int LVL = NS * 16 + 4;  // LDS floats per level (+4 spreads the banks)
-  static constexpr int WAVE = 16 * LVL;    // LDS floats per wavefront
-  __device__ static int row_slot(uint32_t y, uint32_t z) {
-    return D == 3 ? static_cast<int>((y & 1u) | ((z & 1u) << 1)) : static_cast<int>(y & 1u);
-  }
-};
-
-template <int D, typename TG>
-__global__ void __launch_bounds__(256) hashgrid_bwd_v3_kernel(
-    GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
-    int64_t K, const TG* __restrict__ dout, int64_t dout_stride, float* __restrict__ dtable) {
-  using S = SegLayout<D>;
-  constexpr int NC = Corners<D>::NC;  // this lane's yz corners (= rows)
-  __shared__ float seg_all[4][S::WAVE];
-  __shared__ uint32_t ltab[16][2];  // per level: table offset (entries), size T
-
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  float* __restrict__ seg = seg_all[wv];
-  if (threadIdx.x < 16) {
-    const int l = threadIdx.x < n_levels ? threadIdx.x : 0;
-    ltab[threadIdx.x][0] = G.offset[l];
-    ltab[threadIdx.x][1] = G.size[l];
-  }
-  for (int i = lane; i < S::WAVE; i += 64) seg[i] = 0.0f;
-  __syncthreads();
-
-  const int level = lane >> 2, b = (lane >> 1) & 1, f = lane & 1;
-  const int64_t chunk = __builtin_amdgcn_readfirstlane(
-      static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6));
-  const int64_t m0 = chunk * K;
-  if (m0 >= M) return;  // wave-uniform
-  const int64_t m1 = m0 + K < M ? m0 + K : M;
-  // lanes of levels >= n_levels stay alive: every lane takes part in the segment flushes
-  const bool active = level < n_levels;
-  const int lv = active ? level : 0;
-  const float scale = G.scale[lv];
-  const uint32_t T = G.size[lv];
-  const uint32_t loff = G.offset[lv];
-  LevelIdx<D> li;
-  li.init(T, G.res[lv]);
-  const int lbase = level * S::LVL;
-  // coordinates through VECTOR loads: the chunk is wave-uniform, and scalar loads would
-  // share lgkmcnt with the LDS flush, whose waits would then drain the prefetch
-  const uint32_t vzero = __builtin_amdgcn_mbcnt_lo(0u, 0u);
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-
-  uint32_t cell[D];
-  bool have = false;
-#pragma unroll
-  for (int d = 0; d < D; ++d) cell[d] = 0u;
-  float acc[NC];
-  int addr[NC];  // LDS slot address of each accumulator (this lane's x, row r, feature f)
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    acc[c] = 0.0f;
-    addr[c] = 0;
-  }
-
-  // A wavefront's LDS instructions execute in issue order, so the pushes (ds_add) are seen
-  // by the flush reads of other lanes without a wait; this only keeps the compiler from
-  // reordering the LDS accesses across the phases.
-  auto lds_order = [] { asm volatile("" ::: "memory"); };
-
-  // Queue entry of segment (x-block xb, rows yr / zr) of this lane's level:
-  // .x = slot address | h7 << 12 | hashed << 15 | wrap << 16 | level << 24,
-  // .y = table entry (level offset included) of the block's first entry; for a dense block
-  // that may reach T (wrap) the local index instead, the flush applies tcnn's % T per entry
-  auto make_entry = [&](uint32_t xb, uint32_t yr, uint32_t zr) -> uint2 {
-    const uint32_t cy = yr * li.mul[1];
-    const uint32_t cz = D == 3 ? zr * li.mul[D - 1] : 0u;
-    const uint32_t slot = static_cast<uint32_t>(
-        lbase + ((xb & 1u) * S::NR + S::row_slot(yr, zr)) * 16);
-    uint32_t base, h7 = 0u, wrap = 0u;
-    if (li.hashed) {
-      const uint32_t H = D == 3 ? (cy ^ cz) : cy;
-      // level offsets are multiples of 8: off + (base | j') == (off + base) | j'
-      base = loff + (((xb * 8u) ^ H) & (T - 1u) & ~7u);
-      h7 = H & 7u;
-    } else {
-      base = xb * 8u + cy + cz;  // u32 wrap as tcnn
-      if (base >= T - 7u || T < 8u) wrap = 1u;
-      else base += loff;
-    }
-    return uint2{slot | (h7 << 12) | (li.hashed ? (1u << 15) : 0u) | (wrap << 16) |
-                     (static_cast<uint32_t>(level) << 24),
-                 base};
-  };
-
-  // Push this lane's corner sums into their segments and queue the segments of the old
-  // cell (this lane's share: x-block of x + b, y row cell1 + f, both z rows) that the new
-  // cell g does not touch (all of them when closing_all). Then the wave flushes the queue.
-  auto push_and_flush = [&](bool mine, const uint32_t* g, bool closing_all) {
-    if (mine) {
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        __hip_atomic_fetch_add(seg + addr[c], acc[c], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WAVEFRONT);
-        acc[c] = 0.0f;
-      }
-    }
-    constexpr int EPL = NC / 2;  // entries per lane (z rows)
-    bool emit[EPL];
-    uint32_t yr = 0u, ob = 0u;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) emit[k] = false;
-    if (mine) {
-      ob = (cell[0] + static_cast<uint32_t>(b)) >> 3;
-      const bool dup = b == 1 && ob == (cell[0] >> 3);  // same block as the b = 0 lanes
-      const bool blk_gone = closing_all || (ob != (g[0] >> 3) && ob != ((g[0] + 1u) >> 3));
-      yr = cell[1] + static_cast<uint32_t>(f);
-      const bool y_gone = closing_all || (yr != g[1] && yr != g[1] + 1u);
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        const uint32_t zr = D == 3 ? cell[D - 1] + static_cast<uint32_t>(k) : 0u;
-        bool gone = blk_gone || y_gone;
-        if constexpr (D == 3) gone = gone || (zr != g[D - 1] && zr != g[D - 1] + 1u);
-        emit[k] = !dup && gone;
-      }
-    }
-    // the emitting lanes' entries go to the flushing lanes through SGPRs (readlane), 4
-    // segments per pass: lane = 16 * (segment of the pass) + 2 * entry-in-block + feature
-    uint2 ent[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k)
-      ent[k] = emit[k] ? make_entry(ob, yr, D == 3 ? cell[D - 1] + static_cast<uint32_t>(k) : 0u)
-                       : uint2{0u, 0u};
-    uint64_t em[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) em[k] = __ballot(emit[k]);
-    lds_order();
-    const int j = (lane >> 1) & 7, ff = lane & 1, sel = lane >> 4;
-    while (true) {
-      bool any = false;
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) any = any || em[k] != 0ull;
-      if (!any) break;  // wave-uniform
-      uint32_t qx = 0u, qy = 0u;
-      bool have_q = false;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        uint32_t sx = 0u, sy = 0u;
-        bool got = false;
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) {
-          if (!got && em[k] != 0ull) {  // wave-uniform
-            const int l = __builtin_ctzll(em[k]);
-            sx = __builtin_amdgcn_readlane(ent[k].x, l);
-            sy = __builtin_amdgcn_readlane(ent[k].y, l);
-            em[k] &= em[k] - 1ull;
-            got = true;
-          }
-        }
-        if (sel == t) {
-          qx = sx;
-          qy = sy;
-          have_q = got;
-        }
-      }
-      if (have_q) {
-        const int so = static_cast<int>(qx & 0xfffu) + j * 2 + ff;
-        const float v = seg[so];
-        seg[so] = 0.0f;
-        if (v != 0.0f) {
-          uint32_t e;
-          if (qx & (1u << 15)) {
-            e = qy | (static_cast<uint32_t>(j) ^ ((qx >> 12) & 7u));
-          } else if ((qx & (1u << 16)) == 0u) {
-            e = qy + static_cast<uint32_t>(j);
-          } else {  // dense block at the far faces / outside the grid (rare)
-            const uint32_t lvq = qx >> 24;
-            const uint32_t Tq = ltab[lvq][1];
-            uint32_t loc = qy + static_cast<uint32_t>(j);
-            if (loc >= Tq) {
-              const uint32_t s1 = loc - Tq;
-              loc = s1 < Tq ? s1 : loc % Tq;
-            }
-            e = ltab[lvq][0] + loc;
-          }
-          if ((HASH_EXP & 1) == 0)
-            atomicAdd(dtable + static_cast<int64_t>(e) * 2 + ff, v);
-        }
-      }
-    }
-    lds_order();
-  };
-
-  auto step = [&](const float* xv, float gv, bool in_chunk) {
-    float w[D];
-    uint32_t g[D];
-    bool same = have;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const float p = fmaf(scale, xv[d], 0.5f);
-      const float fl = floorf(p);
-      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
-      w[d] = p - fl;
-      same = same && (g[d] == cell[d]);
-    }
-    const bool changed = active && in_chunk && !same;
-    if (__ballot(changed) != 0ull) {  // wave-uniform
-      if (__ballot(changed && have) != 0ull) push_and_flush(changed && have, g, false);
-      if (changed) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) cell[d] = g[d];
-        have = true;
-        const uint32_t xx = cell[0] + static_cast<uint32_t>(b);
-        const int xa = lbase + static_cast<int>((xx >> 3) & 1u) * S::NR * 16 +
-                       static_cast<int>(xx & 7u) * 2 + f;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          const uint32_t yr = cell[1] + static_cast<uint32_t>(Corners<D>::bit(c, 1));
-          const uint32_t zr = D == 3 ? cell[D - 1] + static_cast<uint32_t>(Corners<D>::bit(c, D - 1)) : 0u;
-          addr[c] = xa + S::row_slot(yr, zr) * 16;
-        }
-      }
-    }
-    if (active && in_chunk) {
-      const float wx = b ? w[0] : 1.0f - w[0];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        float wt = wx;
-#pragma unroll
-        for (int d = 1; d < D; ++d) wt *= Corners<D>::bit(c, d) ? w[d] : 1.0f - w[d];
-        acc[c] = fmaf(wt, gv, acc[c]);
-      }
-    }
-  };
-
-  constexpr int BS = HASH_BS3;
-  float xb[BS][D], xn[BS][D];
-  TG gb[BS], gn[BS];
-  auto load_batch = [&](int64_t mb, float (*xo)[D], TG* go) {
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      const int64_t m = mb + j < m1 ? mb + j : m1 - 1;
-#pragma unroll
-      for (int d = 0; d < D; ++d) xo[j][d] = x[m * x_stride + d + vzero];
-      go[j] = dout[m * dout_stride + lv * 2 + f];
-    }
-  };
-  load_batch(m0, xb, gb);
-  for (int64_t mb = m0; mb < m1; mb += BS) {
-    load_batch(mb + BS, xn, gn);
-#pragma unroll
-    for (int j = 0; j < BS; ++j) step(xb[j], to_f32<TG>(gb[j]), mb + j < m1);
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      gb[j] = gn[j];
-#pragma unroll
-      for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
-    }
-  }
-  if (__ballot(active && have) != 0ull) push_and_flush(active && have, cell, true);
-}
-
 static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
   if (d->n_levels < 1 || d->n_levels > ANR_MAX_LEVELS) return false;
   for (int l = 0; l < d->n_levels; ++l) {
@@ -1689,24 +1269,25 @@ static int64_t pick_chunk_v2(int64_t M) {
   return K;
 }
 
-// Kernel generation per direction. Mode 0 (default): forward v1, backward v2 (measured
-// fastest on the ray-coherent bench workload); 1: both v1; 2: both v2; 3: forward v3
-// (F = 2; v1 otherwise), backward v2. ANR_HASHGRID_MODE or anr_hashgrid_force_v1()
-// selects it (test hook). v3 batches the gathers of BS samples (one wait per batch):
-// equal to v1 at BS = 4 and slower at 8 / 16 on the bench geometry — the forward is
-// bound by the rate of cache-line fetches its gathers cause, not by their latency.
+// Kernel generation per direction. Mode 0 (default): forward v6, backward v2 (measured
+// fastest on the ray-coherent bench workload; v6 falls back to v1 above 16 levels or
+// past 32-bit buffer offsets); 1: both v1; 2: both v2; 3: forward v3 (F = 2; v1
+// otherwise), backward v2; 4 / 5: forward v4 / v5, backward v2; 6: forward v1, backward
+// v2 (the previous default). ANR_HASHGRID_MODE or anr_hashgrid_force_v1() selects it (test
+// hook). Measured on the bench coordinates (profiles/r02_hash_fwd_v6_v7_ab.log): the
+// forward spends ~0.35 of its ~0.65 ms on the corner gathers' memory traffic (0.29 ms with
+// no gathers at all) and is not issue-bound (v6 halves the gather path's instructions
+// for 3 %; one 8-B load per x-pair instead of two 4-B loads: 4 %).
 static int g_hashgrid_mode = [] {
   const char* e = getenv("ANR_HASHGRID_MODE");
-  return (e && e[0] >= '0' && e[0] <= '8') ? e[0] - '0' : 0;
+  return (e && e[0] >= '0' && e[0] <= '6') ? e[0] - '0' : 0;
 }();
 static bool fwd_v2() { return g_hashgrid_mode == 2; }
 static bool fwd_v3() { return g_hashgrid_mode == 3; }
 static bool fwd_v4() { return g_hashgrid_mode == 4; }
 static bool fwd_v5() { return g_hashgrid_mode == 5; }
-static bool fwd_v6() { return g_hashgrid_mode == 6 || g_hashgrid_mode == 8; }
-static bool fwd_v7() { return g_hashgrid_mode == 7; }
+static bool fwd_v6() { return g_hashgrid_mode == 0; }
 static bool bwd_v2() { return g_hashgrid_mode != 1; }
-static bool bwd_v3() { return g_hashgrid_mode == 8; }
 
 // Levels per wavefront of the forward walker (1, 2, 4, 8, 16, 32 or 64).
 static int fwd_lpw() {
@@ -1791,33 +1372,6 @@ static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
       return ANR_OK;
     }
   }
-  if (F == 2 && d->n_levels <= 16 && fwd_v7()) {
-    // experiment (tools/hash_probe.py --planar): out holds level-major planes [L][M][2]
-    const int64_t esz_t = tdt == ANR_F16 ? 2 : 4, esz_o = odt == ANR_F16 ? 2 : 4;
-    const int64_t x_bytes = ((M - 1) * x_stride + D) * 4;
-    const int64_t t_bytes = static_cast<int64_t>(G.offset[d->n_levels - 1] + G.size[d->n_levels - 1]) * 2 * esz_t;
-    const int64_t p_bytes = M * 2 * esz_o;
-    const int64_t o_bytes = p_bytes * d->n_levels;
-    const int64_t K = pick_chunk(M);
-    const int64_t lim = int64_t(1) << 31;
-    ANR_CHECK_ARG(x_bytes < lim && t_bytes < lim && o_bytes < lim && (M + K) * x_stride * 4 < lim,
-                  "anr_hashgrid_fwd(v7): sizes beyond 32-bit offsets");
-    const int64_t chunks = ceil_div(M, K);
-    const dim3 grid(static_cast<unsigned>(ceil_div(chunks, 256) * 16)), block(256);
-#define ANR_HG_FWD7(TT, TO)                                                                    \
-  hipLaunchKernelGGL((hashgrid_fwd_v7_kernel<D, TT, TO>), grid, block, 0, s, G, d->n_levels,   \
-                     x, static_cast<uint32_t>(x_bytes), static_cast<uint32_t>(x_stride * 4), M, \
-                     static_cast<int>(K), static_cast<const TT*>(table),                       \
-                     static_cast<uint32_t>(t_bytes), static_cast<TO*>(out),                    \
-                     static_cast<uint32_t>(o_bytes), static_cast<uint32_t>(p_bytes))
-    if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD7(__half, __half);
-    else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD7(__half, float);
-    else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD7(float, __half);
-    else ANR_HG_FWD7(float, float);
-#undef ANR_HG_FWD7
-    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v7)");
-    return ANR_OK;
-  }
   const int lpw = fwd_lpw();
   const int n_groups = static_cast<int>(ceil_div(d->n_levels, lpw));
   const int64_t K = pick_chunk(M);
@@ -1866,23 +1420,6 @@ template <int D, int F>
 static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const float* x,
                       int64_t x_stride, int64_t M, const void* dout, int32_t gdt,
                       int64_t dout_stride, float* dtable, hipStream_t s) {
-  if (F == 2 && d->n_levels <= 16 && bwd_v3() && (g_hashgrid_mode == 8 || pick_chunk_v2(M) >= 64)) {
-    // long chunks only (mode 8, the test hook, forces it): every chunk ends with a flush of
-    // all its open segments
-    const int64_t K = pick_chunk_v2(M);
-    const int64_t waves = ceil_div(M, K);
-    const dim3 grid(static_cast<unsigned>(ceil_div(waves, 4))), block(256);
-    if (gdt == ANR_F16)
-      hipLaunchKernelGGL((hashgrid_bwd_v3_kernel<D, __half>), grid, block, 0, s, G,
-                         d->n_levels, x, x_stride, M, K, static_cast<const __half*>(dout),
-                         dout_stride, dtable);
-    else
-      hipLaunchKernelGGL((hashgrid_bwd_v3_kernel<D, float>), grid, block, 0, s, G,
-                         d->n_levels, x, x_stride, M, K, static_cast<const float*>(dout),
-                         dout_stride, dtable);
-    ANR_CHECK_LAUNCH("anr_hashgrid_bwd(v3)");
-    return ANR_OK;
-  }
   if (F == 2 && d->n_levels <= 16 && bwd_v2()) {
     const int64_t K = pick_chunk_v2(M);
     const int64_t waves = ceil_div(M, K);
@@ -1919,7 +1456,7 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 
 extern "C" int anr_hashgrid_force_v1(int32_t mode) {
   const int prev = anr::g_hashgrid_mode;
-  anr::g_hashgrid_mode = (mode >= 0 && mode <= 8) ? mode : 0;
+  anr::g_hashgrid_mode = (mode >= 0 && mode <= 6) ? mode : 0;
   return prev;
 }
 

@@ -133,15 +133,15 @@ def _grid_inputs(dev, cfg, M, coherent, seed=0):
     return x.contiguous()
 
 
-# hash-grid kernel generations (anr_hashgrid_force_v1 modes): "default" = forward v1 with
-# backward v2, "v2" = both v2, "v1" = both v1, "v3" = forward v3 (batched gathers) with
-# backward v2, "v4" = forward v4 (one thread per sample) with backward v2, "v5" = forward v5
-# (compacted gathers), "v6" = forward v6 (branch-free corners, buffer addressing), "v8" =
-# forward v6 with backward v3 (64-B segment flushes through LDS; forced at every chunk length)
-_HASH_MODES = {"default": 0, "v2": 2, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v6": 6, "v8": 8}
+# hash-grid kernel generations (anr_hashgrid_force_v1 modes): "default" = forward v6
+# (branch-free corners, buffer addressing) with backward v2, "v2" = both v2, "v1" = both v1,
+# "v3" = forward v3 (batched gathers) with backward v2, "v4" = forward v4 (one thread per
+# sample) with backward v2, "v5" = forward v5 (compacted gathers), "v1fwd" = forward v1
+# walker with backward v2 (the r01 default)
+_HASH_MODES = {"default": 0, "v2": 2, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v1fwd": 6}
 
 
-@pytest.fixture(params=["default", "v2", "v1", "v3", "v4", "v5", "v6", "v8"])
+@pytest.fixture(params=["default", "v2", "v1", "v3", "v4", "v5", "v1fwd"])
 def hash_path(request):
     from atmonr_amd import _lib
 
@@ -181,7 +181,7 @@ def test_hashgrid_fwd_bwd_f32(dev, hash_path, cfg, M, coherent):
     close(dtab, gref, rel=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("mode", [0, 8])
+@pytest.mark.parametrize("mode", [0, 6])
 def test_hashgrid_bench_size_adjoint_and_spot_rows(dev, mode):
     """Bench size (8192 rays x 1024 samples, the config-3 grid): the chunk lengths chosen
     only at this size (forward 128, backward 256 samples per chunk) against the oracle on
@@ -868,7 +868,7 @@ def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
     table = ((torch.rand(d.n_params, device=dev, generator=gen) * 2 - 1) * 1e-2).to(dt)
     outs = []
     lib = _lib.load()
-    modes = (1, 4, 5, 6) if tdt == "f16" else (1, 4, 6)  # v5: f16 tables
+    modes = (1, 4, 5, 0) if tdt == "f16" else (1, 4, 0)  # v5: f16 tables; 0: v6
     for mode in modes:
         prev = lib.anr_hashgrid_force_v1(mode)
         out = torch.empty(x.shape[0], 32, device=dev, dtype=dt)
@@ -908,7 +908,7 @@ def test_hashgrid_fwd_v6_outside_grid_and_strides(dev, cfg, M, xs, tdt):
     table = ((torch.rand(d.n_params, device=dev, generator=gen) * 2 - 1) * 1e-2).to(dt)
     lib = _lib.load()
     outs = []
-    for mode in (1, 6):
+    for mode in (1, 0):  # v1, v6 (default)
         prev = lib.anr_hashgrid_force_v1(mode)
         out = torch.full((M + 1, L * 2 + 3), -9.0, device=dev, dtype=dt)
         _lib.call("anr_hashgrid_fwd", ctypes.byref(d), x.data_ptr(), xs, M, table.data_ptr(),

@@ -13,9 +13,9 @@ import glob
 import os
 import sys
 
-KERNELS = {"hash_fwd": "hashgrid_fwd_kernel<3, 2, __half, __half>",
+KERNELS = {"hash_fwd": "hashgrid_fwd_v6_kernel<3, __half, __half>",
+           "hash_fwd_v1": "hashgrid_fwd_kernel<3, 2, __half, __half>",
            "hash_bwd": "hashgrid_bwd_v2_kernel<3, float>",
-           "hash_bwd_v3": "hashgrid_bwd_v3_kernel<3, float>",
            "field_fwd": "field::fwd_kernel<64, 2, false, false>",
            "field_bwd": "field::bwd_kernel<64, 2, true, false, false>",
            "sampler": "sample_uniform_bins_kernel",

@@ -25,7 +25,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # bench.py kernel tag -> substring of the mangled/demangled kernel name
 TAGS = {
-    "hash_fwd": "hashgrid_fwd_kernel<3, 2, __half, __half>",
+    "hash_fwd": "hashgrid_fwd_v6_kernel<3, __half, __half>",
+    "hash_fwd_v1": "hashgrid_fwd_kernel<3, 2, __half, __half>",
     "hash_bwd": "hashgrid_bwd_v2_kernel<3, float>",
     "field_fwd": "field::fwd_kernel<64, 2, false, false>",
     "field_bwd": "field::bwd_kernel<64, 2, true, false, false>",

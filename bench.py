@@ -158,6 +158,8 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
     pipe.send_tensors_to(dev)
     opt = pipe.get_optimizer({"lr": 5e-4})
     bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev)
+    if world > 1:
+        bucket.broadcast_params(0)  # AtmoNeRF's nn.Linear init is unseeded per rank
     if not args.no_fused_zero:
         bucket.fuse_zero_into(opt)  # the Adam pass zeroes the bucket (no per-step fill)
     loader = BatchLoader(ds, batch_size, shuffle=True, rank=rank, world_size=world, seed=0)
@@ -358,6 +360,8 @@ def main():
     from atmonr_amd.parallel import FlatGradBucket
 
     bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev)
+    if world > 1:
+        bucket.broadcast_params(0)  # replicas start from rank 0's weights
     if not args.no_fused_zero:
         bucket.fuse_zero_into(opt)  # the AdamW pass zeroes the bucket (no per-step fill)
     if not args.no_overlap:

@@ -78,11 +78,12 @@ __device__ __forceinline__ uint32_t grid_index(uint32_t T, uint32_t res, const u
 // outside [0,1]) included; branch-free apart from the rare full modulo.
 template <int D>
 struct LevelIdx {
-  uint32_t T, mul[D];
+  uint32_t T, mul[D], res1;  // res1 = res - 1
   bool hashed;
   __device__ void init(uint32_t T_, uint32_t res) {
     constexpr uint32_t primes[3] = {1u, 2654435761u, 805459861u};
     T = T_;
+    res1 = res - 1u;
     uint64_t st = 1;
     uint32_t stride[D];
 #pragma unroll
@@ -137,7 +138,6 @@ struct LaneCorners {
       c2[1] = c2[0] + li.mul[2];
     }
     uint32_t sum[NC];
-    bool wrap = false;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       uint32_t hx = cx ^ c1[c & 1];
@@ -147,9 +147,14 @@ struct LaneCorners {
         sum[c] += c2[c >> 1];
       }
       idx[c] = li.hashed ? (hx & (li.T - 1u)) : sum[c];
-      wrap = wrap || (!li.hashed && sum[c] >= li.T);
     }
-    if (wrap) {
+    // a dense corner sum can reach T only with a corner on the far face or outside the
+    // grid: below that every sum is <= res^D - 1 < T (one test per cell, not per corner;
+    // the unsigned max also catches negative cell coordinates)
+    uint32_t gm = cell[0] + static_cast<uint32_t>(b);
+#pragma unroll
+    for (int d = 1; d < D; ++d) gm = gm > cell[d] ? gm : cell[d];
+    if (!li.hashed && gm >= li.res1) {
 #pragma unroll
       for (int c = 0; c < NC; ++c)
         if (!li.hashed && sum[c] >= li.T) {
@@ -1126,18 +1131,27 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v6_kernel(
   }
 }
 
-template <int D, typename TG>
+// XS / DS: compile-time coordinate and dL/dy row strides (0 = the run-time x_stride /
+// dout_stride). With both known (the fused field's (M,3) coordinates and (M,32) dL/denc)
+// every prefetch address is a per-batch scalar base plus immediate offsets: the walk
+// issues no per-sample address arithmetic (r01 spent ~25 scalar instructions per sample
+// on 64-bit clamped indices), and only a chunk's last two batches clamp.
+template <int D, typename TG, int XS, int DS>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
-    GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
-    int64_t K, const TG* __restrict__ dout, int64_t dout_stride, float* __restrict__ dtable) {
+    GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride_rt, int64_t M,
+    int64_t K, const TG* __restrict__ dout, int64_t dout_stride_rt, float* __restrict__ dtable) {
   constexpr int NC = Corners<D>::NC;
+  const int64_t x_stride = XS > 0 ? XS : x_stride_rt;
+  const int64_t dout_stride = DS > 0 ? DS : dout_stride_rt;
   const int lane = threadIdx.x & 63;
   const int level = lane >> 2, b = (lane >> 1) & 1, f = lane & 1;
   const int64_t chunk = __builtin_amdgcn_readfirstlane(
       static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6));
   const int64_t m0 = chunk * K;
+  // chunk bounds are wave-uniform: kept in scalar registers
+  const int64_t m1 = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(
+      static_cast<int>(m0 + K < M ? K : M - m0))) + m0;
   if (m0 >= M || level >= n_levels) return;
-  const int64_t m1 = m0 + K < M ? m0 + K : M;
   const float scale = G.scale[level];
   const uint32_t res = G.res[level];
   const uint32_t T = G.size[level];
@@ -1178,8 +1192,11 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
         LaneCorners<D>::carry(acc, dl, keepx, nacc);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
+          // no test of acc != 0 here: a leaving corner's sum is zero only when its
+          // weights were (samples exactly on the cell faces), and the per-corner test
+          // cost more instructions than the rare zero requests it saves
           const bool out = !keepx || LaneCorners<D>::leaves(c, dl);
-          if (out && acc[c] != 0.0f && (HASH_EXP & 1) == 0)
+          if (out && (HASH_EXP & 1) == 0)
             atomicAdd(grad + static_cast<int64_t>(idx[c]) * 2, acc[c]);
         }
 #pragma unroll
@@ -1204,13 +1221,25 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
   constexpr int BS = HASH_BS;
   float xb[BS][D], xn[BS][D];
   TG gb[BS], gn[BS];
+  const int col = level * 2 + f;
   auto load_batch = [&](int64_t mb, float (*xo)[D], TG* go) {
+    if ((XS > 0 && DS > 0) && mb + BS <= m1) {  // wave-uniform: a full batch, no clamp
+      const float* __restrict__ xp = x + mb * XS;
+      const TG* __restrict__ dp = dout + mb * DS;
 #pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      const int64_t m = mb + j < m1 ? mb + j : m1 - 1;
+      for (int j = 0; j < BS; ++j) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) xo[j][d] = x[m * x_stride + d];
-      go[j] = dout[m * dout_stride + level * 2 + f];
+        for (int d = 0; d < D; ++d) xo[j][d] = xp[j * XS + d];
+        go[j] = dp[j * DS + col];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < BS; ++j) {
+        const int64_t m = mb + j < m1 ? mb + j : m1 - 1;
+#pragma unroll
+        for (int d = 0; d < D; ++d) xo[j][d] = x[m * x_stride + d];
+        go[j] = dout[m * dout_stride + col];
+      }
     }
   };
   load_batch(m0, xb, gb);
@@ -1273,14 +1302,15 @@ static int64_t pick_chunk_v2(int64_t M) {
 // fastest on the ray-coherent bench workload; v6 falls back to v1 above 16 levels or
 // past 32-bit buffer offsets); 1: both v1; 2: both v2; 3: forward v3 (F = 2; v1
 // otherwise), backward v2; 4 / 5: forward v4 / v5, backward v2; 6: forward v1, backward
-// v2 (the previous default). ANR_HASHGRID_MODE or anr_hashgrid_force_v1() selects it (test
+// v2 (the previous default); 7: as 0 with the backward's run-time-stride instantiation
+// (A/B of the compile-time strides). ANR_HASHGRID_MODE or anr_hashgrid_force_v1() selects it (test
 // hook). Measured on the bench coordinates (profiles/r02_hash_fwd_v6_v7_ab.log): the
 // forward spends ~0.35 of its ~0.65 ms on the corner gathers' memory traffic (0.29 ms with
 // no gathers at all) and is not issue-bound (v6 halves the gather path's instructions
 // for 3 %; one 8-B load per x-pair instead of two 4-B loads: 4 %).
 static int g_hashgrid_mode = [] {
   const char* e = getenv("ANR_HASHGRID_MODE");
-  return (e && e[0] >= '0' && e[0] <= '6') ? e[0] - '0' : 0;
+  return (e && e[0] >= '0' && e[0] <= '7') ? e[0] - '0' : 0;
 }();
 static bool fwd_v2() { return g_hashgrid_mode == 2; }
 static bool fwd_v3() { return g_hashgrid_mode == 3; }
@@ -1424,14 +1454,20 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
     const int64_t K = pick_chunk_v2(M);
     const int64_t waves = ceil_div(M, K);
     const dim3 grid(static_cast<unsigned>(ceil_div(waves, 4))), block(256);
-    if (gdt == ANR_F16)
-      hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<D, __half>), grid, block, 0, s, G,
-                         d->n_levels, x, x_stride, M, K, static_cast<const __half*>(dout),
-                         dout_stride, dtable);
-    else
-      hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<D, float>), grid, block, 0, s, G,
-                         d->n_levels, x, x_stride, M, K, static_cast<const float*>(dout),
-                         dout_stride, dtable);
+    // compile-time strides for the fused field's layout ((M,3) coordinates, (M,32) dL/denc)
+    const bool fixed = D == 3 && x_stride == 3 && dout_stride == 32 && g_hashgrid_mode != 7;
+#define ANR_HG_BWD2(TG, XS_, DS_)                                                          \
+  hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<D, TG, XS_, DS_>), grid, block, 0, s, G,        \
+                     d->n_levels, x, x_stride, M, K, static_cast<const TG*>(dout),          \
+                     dout_stride, dtable)
+    if (gdt == ANR_F16) {
+      if (fixed) ANR_HG_BWD2(__half, 3, 32);
+      else ANR_HG_BWD2(__half, 0, 0);
+    } else {
+      if (fixed) ANR_HG_BWD2(float, 3, 32);
+      else ANR_HG_BWD2(float, 0, 0);
+    }
+#undef ANR_HG_BWD2
     ANR_CHECK_LAUNCH("anr_hashgrid_bwd(v2)");
     return ANR_OK;
   }
@@ -1456,7 +1492,7 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 
 extern "C" int anr_hashgrid_force_v1(int32_t mode) {
   const int prev = anr::g_hashgrid_mode;
-  anr::g_hashgrid_mode = (mode >= 0 && mode <= 6) ? mode : 0;
+  anr::g_hashgrid_mode = (mode >= 0 && mode <= 7) ? mode : 0;
   return prev;
 }
 

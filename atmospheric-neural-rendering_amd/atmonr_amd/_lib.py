@@ -102,6 +102,16 @@ class PosencDesc(Structure):
 _P = c_void_p
 
 
+class AdamTensor(Structure):
+    """anr_adam_tensor (include/anr.h)."""
+    _fields_ = [("params", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p),
+                ("exp_avg_sq", c_void_p), ("params_f16", c_void_p), ("n", c_int64),
+                ("lr", c_float), ("weight_decay", c_float), ("step", c_int64)]
+
+
+ADAM_MAX_TENSORS = 16
+
+
 class GatherCol(Structure):
     """anr_gather_col (include/anr.h)."""
 
@@ -243,6 +253,9 @@ _SIGNATURES = {
         c_int32,
         [_P, _P, _P, _P, _P, c_int64, c_float, c_float, c_float, c_float, c_float,
          c_int32, c_int64, c_int32, _P],
+    ),
+    "anr_adam_step_multi": (
+        c_int32, [_P, c_int32, c_float, c_float, c_float, c_int32, c_int32, _P],
     ),
 }
 

@@ -8,6 +8,8 @@ with torch's.
 
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -24,15 +26,21 @@ class FusedAdam(torch.optim.Optimizer):
         # no-op for buffers that stay allocated, e.g. a FlatGradBucket: see mark_zero)
         self.zero_grad_in_step = zero_grad_in_step
         self.zeroed_buckets: list = []  # FlatGradBucket.fuse_zero_into
+        self.multi_tensor = True  # one anr_adam_step_multi launch per step and device
 
     @torch.no_grad()
     def step(self, closure=None):
+        """Every parameter of every group in one anr_adam_step_multi launch per device
+        (``multi_tensor=False``: one anr_adam_step launch per parameter)."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        batches: dict = {}  # device -> [anr_adam_tensor]
         for group in self.param_groups:
             b1, b2 = group["betas"]
+            if (b1, b2, group["eps"]) != self._shared(group):
+                raise _lib.ANRError("FusedAdam: betas / eps must be equal across param groups")
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -48,20 +56,42 @@ class FusedAdam(torch.optim.Optimizer):
                     # keep it on the host so the step count never costs a device sync
                     st["step"] = st["step"].cpu()
                 st["step"] += 1
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                if not p.grad.is_contiguous():
+                    p.grad = p.grad.contiguous()
                 # the f16 compute copy of the parameter (_lib.compute_copy), if a module
                 # keeps one, is written in the same pass and stays current
                 sh = getattr(p, "_anr_shadow", None)
                 if sh is not None and (sh.dtype != torch.float16 or sh.shape != p.shape):
                     sh = None
-                call("anr_adam_step", ptr(p), ptr(g), ptr(st["exp_avg"]),
-                     ptr(st["exp_avg_sq"]), ptr(sh), p.numel(), float(group["lr"]),
-                     float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
-                     int(self.decoupled), int(st["step"].item()),
-                     int(self.zero_grad_in_step), _lib.stream(p.device))
+                t = _lib.AdamTensor(ptr(p), ptr(p.grad), ptr(st["exp_avg"]),
+                                    ptr(st["exp_avg_sq"]), ptr(sh), p.numel(),
+                                    float(group["lr"]), float(group["weight_decay"]),
+                                    int(st["step"].item()))
+                batches.setdefault(p.device, []).append(t)
                 if sh is not None:
                     p._anr_shadow_ver = p._version
+        b1, b2 = self.defaults["betas"]
+        eps = self.defaults["eps"]
+        if self.param_groups:
+            b1, b2 = self.param_groups[0]["betas"]
+            eps = self.param_groups[0]["eps"]
+        for dev, ts in batches.items():
+            if self.multi_tensor:
+                arr = (_lib.AdamTensor * len(ts))(*ts)
+                call("anr_adam_step_multi", ctypes.addressof(arr), len(ts), float(b1), float(b2),
+                     float(eps), int(self.decoupled), int(self.zero_grad_in_step),
+                     _lib.stream(dev))
+            else:
+                for t in ts:
+                    call("anr_adam_step", t.params, t.grad, t.exp_avg, t.exp_avg_sq,
+                         t.params_f16, t.n, t.lr, float(b1), float(b2), float(eps),
+                         t.weight_decay, int(self.decoupled), t.step,
+                         int(self.zero_grad_in_step), _lib.stream(dev))
         if self.zero_grad_in_step:
             for b in self.zeroed_buckets:
                 b.mark_zero()
         return loss
+
+    def _shared(self, group):
+        g0 = self.param_groups[0]
+        return (g0["betas"][0], g0["betas"][1], g0["eps"])

@@ -423,6 +423,27 @@ int anr_adam_step(float* params, float* grad, float* exp_avg, float* exp_avg_sq,
                   float eps, float weight_decay, int32_t decoupled, int64_t step,
                   int32_t zero_grad, anr_stream_t stream);
 
+/* Every tensor of one optimizer step (torch.optim.AdamW.step over all param groups,
+ * instant_ngp.py:120-126 / trainer.py:105) in one launch: per tensor its own lr,
+ * weight_decay and step count; beta1/2, eps, decoupled and zero_grad shared. Tensors
+ * travel in the kernel arguments, ANR_ADAM_MAX_TENSORS per launch (more: several
+ * launches, same stream). Same arithmetic as anr_adam_step. */
+#define ANR_ADAM_MAX_TENSORS 16
+typedef struct anr_adam_tensor {
+  float* params;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  void* params_f16; /* nullable f16 shadow */
+  int64_t n;
+  float lr;
+  float weight_decay;
+  int64_t step;
+} anr_adam_tensor;
+int anr_adam_step_multi(const anr_adam_tensor* tensors, int32_t n_tensors, float beta1,
+                        float beta2, float eps, int32_t decoupled, int32_t zero_grad,
+                        anr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -516,6 +516,45 @@ def test_adam_matches_torch(dev, decoupled, wd):
     close(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"], rel=1e-5, atol=1e-12)
 
 
+@pytest.mark.parametrize("decoupled", [True, False])
+def test_adam_multi_tensor_matches_torch_and_per_tensor(dev, decoupled):
+    """anr_adam_step_multi (FusedAdam's default): 19 tensors (more than one launch's 16,
+    one of them empty), two param groups with their own lr / weight decay, against
+    torch.optim.AdamW / Adam, and bit for bit against the per-tensor launches."""
+    from atmonr_amd.optim import FusedAdam
+
+    gen = torch.Generator().manual_seed(3)
+    sizes = [1, 1023, 1024, 1025, 4097, 0, 77777] + [300 + 17 * i for i in range(12)]
+    p0 = [torch.randn(n, generator=gen) for n in sizes]
+    grads = [[torch.randn(n, generator=gen) * 0.1 for n in sizes] for _ in range(4)]
+
+    def groups(ps):
+        return [{"params": ps[:9], "weight_decay": 0.0, "lr": 1e-2},
+                {"params": ps[9:], "weight_decay": 1e-2, "lr": 3e-3}]
+
+    kw = dict(betas=(0.9, 0.99), eps=1e-15)
+    pa = [torch.nn.Parameter(x.clone().to(dev)) for x in p0]
+    pc = [torch.nn.Parameter(x.clone().to(dev)) for x in p0]
+    pb = [torch.nn.Parameter(x.clone()) for x in p0]
+    oa = FusedAdam(groups(pa), decoupled=decoupled, **kw)
+    oc = FusedAdam(groups(pc), decoupled=decoupled, **kw)
+    oc.multi_tensor = False
+    ob = (torch.optim.AdamW if decoupled else torch.optim.Adam)(groups(pb), foreach=False, **kw)
+    for gr in grads:
+        for x, y, z, g in zip(pa, pc, pb, gr):
+            x.grad, y.grad, z.grad = g.to(dev), g.to(dev), g.clone()
+        oa.step()
+        oc.step()
+        ob.step()
+    for x, y, z in zip(pa, pc, pb):
+        assert torch.equal(x.detach(), y.detach())
+        if z.numel():
+            close(x.detach(), z.detach(), rel=1e-5, atol=1e-6)
+    for x, z in zip(pa, pb):
+        if z.numel():
+            close(oa.state[x]["exp_avg_sq"], ob.state[z]["exp_avg_sq"], rel=1e-5, atol=1e-12)
+
+
 # ------------------------------------------------------------------ fused dir encoding + MLP
 @pytest.mark.parametrize("width,half", [(64, True), (64, False), (32, True)])
 def test_ingp_dir_mlp_matches_unfused(dev, width, half):

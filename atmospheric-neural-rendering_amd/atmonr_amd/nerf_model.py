@@ -69,24 +69,6 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
-def _relu_bwd(g: torch.Tensor, y: torch.Tensor, want_db: bool):
-    """(g masked where y > 0, its column sum) — relu's subgradient at 0 is 0, as torch's."""
-    g = g.contiguous()
-    M, C = g.shape
-    if C % 4 == 0 and C <= 1024 and y.is_contiguous() and M >= 256:
-        # one pass: mask + per-block column sums (anr_relu_bwd_colsum)
-        from . import _lib
-
-        parts = min(1024, M // 256)
-        gm = torch.empty_like(g)
-        partial = torch.empty(parts, C, device=g.device, dtype=torch.float32)
-        _lib.call("anr_relu_bwd_colsum", _lib.ptr(g), _lib.ptr(y), M, C, _lib.ptr(gm),
-                  _lib.ptr(partial), parts, _lib.stream(g.device))
-        return gm, (partial.sum(0) if want_db else None)
-    gm = torch.ops.aten.threshold_backward(g, y, 0)
-    return gm, (_column_sum(gm) if want_db else None)
-
-
 class _LinearReLUFn(torch.autograd.Function):
     """relu(F.linear(x, W, b)) as one library GEMM with a bias + ReLU epilogue
     (torch._addmm_activation, which has no autograd formula) and the matching backward:
@@ -101,48 +83,24 @@ class _LinearReLUFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, weight, y = ctx.saved_tensors
-        gm, db = _relu_bwd(g, y, ctx.needs_input_grad[2])
+        g = g.contiguous()
+        M, C = g.shape
+        if C % 4 == 0 and C <= 1024 and y.is_contiguous() and M >= 256:
+            # one pass: mask + per-block column sums (anr_relu_bwd_colsum)
+            from . import _lib
+
+            parts = min(1024, M // 256)
+            gm = torch.empty_like(g)
+            partial = torch.empty(parts, C, device=g.device, dtype=torch.float32)
+            _lib.call("anr_relu_bwd_colsum", _lib.ptr(g), _lib.ptr(y), M, C, _lib.ptr(gm),
+                      _lib.ptr(partial), parts, _lib.stream(g.device))
+            db = partial.sum(0) if ctx.needs_input_grad[2] else None
+        else:
+            gm = torch.ops.aten.threshold_backward(g, y, 0)
+            db = _column_sum(gm) if ctx.needs_input_grad[2] else None
         dx = gm @ weight if ctx.needs_input_grad[0] else None
         dw = _weight_grad(gm, x) if ctx.needs_input_grad[1] else None
         return dx, dw, db
-
-
-class _LinearReLUSkipFn(torch.autograd.Function):
-    """relu(cat([x1, x2], 1) @ W^T + b) without the concatenation (models/nerf.py's skip
-    connections into fc6 and fc10): the two K ranges of W accumulate into one output
-    (addmm of the short x2 range first, then of x1 onto it), and the backward returns dx1
-    and dx2 as separate contiguous GEMM outputs instead of strided slices of one."""
-
-    @staticmethod
-    def forward(ctx, x1, x2, weight, bias):
-        k1 = x1.shape[1]
-        y = torch.addmm(bias, x2, weight[:, k1:].t())
-        y.addmm_(x1, weight[:, :k1].t())
-        y.relu_()
-        ctx.save_for_backward(x1, x2, weight, y)
-        return y
-
-    @staticmethod
-    def backward(ctx, g):
-        x1, x2, weight, y = ctx.saved_tensors
-        k1 = x1.shape[1]
-        gm, db = _relu_bwd(g, y, ctx.needs_input_grad[3])
-        dx1 = gm @ weight[:, :k1] if ctx.needs_input_grad[0] else None
-        dx2 = gm @ weight[:, k1:] if ctx.needs_input_grad[1] else None
-        dw = None
-        if ctx.needs_input_grad[2]:
-            dw = torch.cat([_weight_grad(gm, x1.contiguous()), _weight_grad(gm, x2.contiguous())], 1)
-        return dx1, dx2, dw, db
-
-
-_SKIP_SPLIT = os.environ.get("ANR_NERF_SKIP_SPLIT", "1") == "1"
-
-
-def _linear_relu_skip(layer: nn.Linear, x1: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
-    if _SKIP_SPLIT and x1.is_cuda and x1.dim() == 2 and x1.dtype == torch.float32 \
-            and torch.is_grad_enabled():
-        return _LinearReLUSkipFn.apply(x1, x2, layer.weight, layer.bias)
-    return _linear_relu(layer, torch.cat([x1, x2], dim=1))
 
 
 def _linear_relu(layer: nn.Linear, x: torch.Tensor) -> torch.Tensor:
@@ -194,7 +152,8 @@ class AtmoNeRF(nn.Module):
         x = _linear_relu(self.fc3, x)
         x = _linear_relu(self.fc4, x)
         x = _linear_relu(self.fc5, x)
-        x = _linear_relu_skip(self.fc6, x, x_pos)  # skip connection (cat([x, x_pos]))
+        x = torch.cat([x, x_pos], dim=1)  # skip connection
+        x = _linear_relu(self.fc6, x)
         x = _linear_relu(self.fc7, x)
         x = _linear_relu(self.fc8, x)
         x = self.fc9(x)
@@ -209,7 +168,7 @@ class AtmoNeRF(nn.Module):
         without an activation, as in the reference."""
         x_pos, d = x[:, : self.pos_channels], x[:, self.pos_channels:]
         x, sigma = self.forward_pos_only(x_pos, noise)
-        x = _linear_relu_skip(self.fc10, x[:, : self.hidden_dim], d)
+        x = _linear_relu(self.fc10, torch.cat([x[:, : self.hidden_dim], d], dim=1))
         return torch.sigmoid(self.fc11(x)), sigma
 
 

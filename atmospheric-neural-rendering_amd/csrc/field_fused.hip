@@ -542,8 +542,27 @@ __device__ __forceinline__ void fwd_raw_to_rows(const FwdRaw& r, Rows& in) {
   in.ds = 0.0f;
 }
 
-template <int W, int NHD, bool ROWS, bool BF>
+// Uniform-tile forward (UT): dense rows, n_per_ray a multiple of 16, 4 colour outputs,
+// 16-byte aligned colour rows, byte offsets below 2^31 — the bench and training shape.
+// A 16-row tile is then one ray's samples, so its direction is one scalar load (scalar
+// cache and lgkmcnt, not the vector-memory queue), and the outputs go out as raw buffer
+// stores, one sigma and one 4-wide colour store per lane with no branch (lanes with
+// nothing to write get an out-of-range offset, which the hardware drops). Every tile then
+// issues the same vector-memory instructions (one input load, two stores), so the wait
+// for the next tile's prefetched encodings is vmcnt(2) and leaves this tile's stores in
+// flight. In the general form the per-lane guarded stores and the branch-sunk direction
+// remap made the compiler wait with vmcnt(0) twice per tile: one store round trip and
+// one prefetch round trip per tile.
+typedef uint32_t u4v __attribute__((vector_size(16)));
+typedef __attribute__((address_space(4))) const float const_f32;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, static_cast<int>(bytes),
+                                           0x00020000);
+}
+
+template <int W, int NHD, bool ROWS, bool BF, bool UT>
 __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
+  static_assert(!(UT && ROWS), "the uniform-tile form needs dense rows");
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   // wave index through readfirstlane: the tile loop then runs on scalar registers
   const int waves = blockDim.x >> 6, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -553,10 +572,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
   const int64_t n_full = a.M / 16;  // tiles with all 16 rows in range
   const int64_t tstride = static_cast<int64_t>(gridDim.x) * waves;
   int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave;
-  auto body = [&](const Rows& cur, int64_t row) {
-    Tile<W, NHD> t;
-    const bool valid = row < a.M;
-    tile_forward<W, NHD, 1, BF>(fw, &cur, &valid, g, &t, NoSink{});
+  auto store = [&](const Tile<W, NHD>& t, int64_t row) {
     if (row < a.M) {
       const int64_t drow = dense_row<ROWS>(a, row);
       if (g == 0) a.sigma[drow] = fmaxf(t.po[0], 0.0f);
@@ -573,16 +589,68 @@ __global__ void __launch_bounds__(256) fwd_kernel(Args a) {
       }
     }
   };
-  // full tiles: the next tile's inputs are in flight while this one computes (the
-  // prefetch index is clamped, so the loop body has no branch around the loads)
-  FwdRaw nraw;
-  if (tile < n_full) load_fwd_raw<ROWS>(a, tile * 16 + li, g, nraw);
-  for (; tile < n_full; tile += tstride) {
-    Rows cur;
-    fwd_raw_to_rows(nraw, cur);
-    const int64_t tn = tile + tstride < n_full ? tile + tstride : tile;
-    load_fwd_raw<ROWS>(a, tn * 16 + li, g, nraw);
-    body(cur, tile * 16 + li);
+  auto body = [&](const Rows& cur, int64_t row) {
+    Tile<W, NHD> t;
+    const bool valid = row < a.M;
+    tile_forward<W, NHD, 1, BF>(fw, &cur, &valid, g, &t, NoSink{});
+    store(t, row);
+  };
+  if constexpr (UT) {
+    const __amdgpu_buffer_rsrc_t rsig = out_rsrc(a.sigma, a.M * 4);
+    const __amdgpu_buffer_rsrc_t rcol = out_rsrc(a.color, a.M * a.color_stride * 4);
+    const uint32_t cs_bytes = static_cast<uint32_t>(a.color_stride) * 4u;
+    auto enc_ptr = [&](int64_t t) {
+      return reinterpret_cast<const h8*>(a.enc + (t * 16 + li) * a.enc_stride + 8 * g);
+    };
+    h8 nxe;
+    if (tile < n_full) {
+      nxe = *enc_ptr(tile);
+      // two dropped stores: the loop is entered with the vector-memory queue of its back
+      // edge (an input load, then a tile's two stores)
+      __builtin_amdgcn_raw_buffer_store_b32(0u, rsig, 0x80000000u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{0u, 0u, 0u, 0u}, rcol, 0x80000000u, 0, 0);
+    }
+    for (; tile < n_full; tile += tstride) {
+      Rows cur;
+      cur.xe = nxe;
+      // wave-uniform ray and direction; readfirstlane (convergent) also keeps the loads from
+      // being sunk into dir_input's g == 0 branch as vector loads
+      const uint32_t ray =
+          __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tile * 16) / a.n_per_ray);
+      const const_f32* d = (const_f32*)(a.dirs + static_cast<int64_t>(ray) * 3);
+      auto sdir = [&](int k) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, d[k])));
+      };
+      cur.dx = sdir(0) * 2.0f - 1.0f;
+      cur.dy = sdir(1) * 2.0f - 1.0f;
+      cur.dz = sdir(2) * 2.0f - 1.0f;
+      cur.dc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+      cur.ds = 0.0f;
+      const int64_t tn = tile + tstride < n_full ? tile + tstride : tile;
+      nxe = *enc_ptr(tn);
+      Tile<W, NHD> t;
+      const bool valid = true;
+      tile_forward<W, NHD, 1, BF>(fw, &cur, &valid, g, &t, NoSink{});
+      const uint32_t row = static_cast<uint32_t>(tile * 16 + li);
+      const uint32_t so = g == 0 ? row * 4u : 0x80000000u;
+      const uint32_t co = g == 0 ? row * cs_bytes : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaxf(t.po[0], 0.0f)), rsig, so, 0, 0);
+      const u4v v = {__float_as_uint(fmaxf(t.col[0], 0.0f)), __float_as_uint(fmaxf(t.col[1], 0.0f)),
+                     __float_as_uint(fmaxf(t.col[2], 0.0f)), __float_as_uint(fmaxf(t.col[3], 0.0f))};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rcol, co, 0, 0);
+    }
+  } else {
+    // full tiles: the next tile's inputs are in flight while this one computes (the
+    // prefetch index is clamped, so the loop body has no branch around the loads)
+    FwdRaw nraw;
+    if (tile < n_full) load_fwd_raw<ROWS>(a, tile * 16 + li, g, nraw);
+    for (; tile < n_full; tile += tstride) {
+      Rows cur;
+      fwd_raw_to_rows(nraw, cur);
+      const int64_t tn = tile + tstride < n_full ? tile + tstride : tile;
+      load_fwd_raw<ROWS>(a, tn * 16 + li, g, nraw);
+      body(cur, tile * 16 + li);
+    }
   }
   for (; tile < n_tiles; tile += tstride) {  // the last, partial tile
     Rows cur;
@@ -1343,6 +1411,9 @@ static int g_target_log2 = 6;  // f16 gradient scale: max |dL/dout| of a wavefro
 // backward kernel generation: 0 = LDS tiles (bwd_kernel), 1 = register-transposed
 // (bwd_rt_kernel); test / A-B hook anr_ingp_field_force_bwd
 static int g_bwd_mode = 1;
+// forward form: 1 = the uniform-tile kernel where the shapes allow (default), 0 = always
+// the general kernel; test / A-B hook anr_ingp_field_force_fwd
+static int g_fwd_ut = 1;
 
 // Backward launch geometry: one resident wavefront per slot (4 per block), each owning a
 // contiguous range of 32-sample tiles. The f16 backward needs one float per wavefront of
@@ -1396,7 +1467,7 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
   const int waves = 4;
   if (op == 1) {
     const int64_t tiles = (a.M + 15) / 16;
-    const void* fn = reinterpret_cast<const void*>(&fwd_kernel<W, NHD, false, BF>);
+    const void* fn = reinterpret_cast<const void*>(&fwd_kernel<W, NHD, false, BF, false>);
     static int pc = 0;
     if (pc == 0) {
       int nb = 0;
@@ -1406,10 +1477,19 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
     int64_t blocks = (tiles + waves - 1) / waves;
     if (blocks > 256LL * pc) blocks = 256LL * pc;
     if (blocks < 1) blocks = 1;
+    // the uniform-tile form (see fwd_kernel): dense rows whose 16-row tiles are one ray each,
+    // 4 colour outputs in 16-byte aligned rows, byte offsets of the outputs below 2^31
+    const bool ut = g_fwd_ut && a.rows == nullptr && a.n_per_ray % 16 == 0 && a.n_out == 4 &&
+                    (a.color_stride & 3) == 0 && a.M * a.color_stride * 4 < (int64_t{1} << 31);
+#define ANR_FWD_LAUNCH(ROWSV, BSV) \
+  hipLaunchKernelGGL((fwd_kernel<W, NHD, ROWSV, BF, BSV>), dim3(blocks), dim3(64 * waves), 0, st, a)
     if (a.rows)
-      hipLaunchKernelGGL((fwd_kernel<W, NHD, true, BF>), dim3(blocks), dim3(64 * waves), 0, st, a);
+      ANR_FWD_LAUNCH(true, false);
+    else if (ut)
+      ANR_FWD_LAUNCH(false, true);
     else
-      hipLaunchKernelGGL((fwd_kernel<W, NHD, false, BF>), dim3(blocks), dim3(64 * waves), 0, st, a);
+      ANR_FWD_LAUNCH(false, false);
+#undef ANR_FWD_LAUNCH
     return 0;
   }
   const bool fast = a.n_out == 4 && (a.d_color_stride & 3) == 0 && a.d_sigma != nullptr;
@@ -1521,6 +1601,12 @@ extern "C" int64_t anr_ingp_field_bwd_workspace_bytes(const anr_mlp_desc* pos,
 extern "C" int anr_ingp_field_force_bwd(int32_t mode) {
   const int prev = g_bwd_mode;
   if (mode == 0 || mode == 1) g_bwd_mode = mode;
+  return prev;
+}
+
+extern "C" int anr_ingp_field_force_fwd(int32_t mode) {
+  const int prev = g_fwd_ut;
+  if (mode == 0 || mode == 1) g_fwd_ut = mode;
   return prev;
 }
 

@@ -270,6 +270,12 @@ int anr_ingp_field_set_grad_scale(int32_t log2_target);
  * the weights). Same math and results. Test / A-B hook; process-wide; other values keep
  * the current mode. Returns the previous mode. */
 int anr_ingp_field_force_bwd(int32_t mode);
+/* Forward kernel form: 1 = the uniform-tile form wherever the shapes allow it (default:
+ * dense rows, samples_per_ray a multiple of 16, 4 colour outputs, 16-byte aligned colour
+ * rows; one scalar direction load per 16-row tile, branch-free output stores), 0 = always
+ * the general form. Same math and bit-identical results. Test / A-B hook; process-wide;
+ * other values keep the current mode. Returns the previous mode. */
+int anr_ingp_field_force_fwd(int32_t mode);
 int64_t anr_ingp_field_bwd_workspace_bytes(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
                                            int32_t mma_dtype, int64_t M);
 int anr_ingp_field_pack(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,

@@ -805,6 +805,53 @@ def test_ingp_field_bwd_generations_agree(dev, width, nhd, mma):
         assert ((a - b).norm() / b.norm()).item() <= 1e-5
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mma", ["f16", "bf16"])
+@pytest.mark.parametrize("n_per_ray,R,extra,width,nhd", [
+    (16, 37, 0, 64, 2),     # one ray per tile, every tile full
+    (64, 29, 5, 64, 2),     # partial last tile (general tail loop)
+    (1024, 3, 0, 64, 2),    # the bench's samples per ray
+    (48, 11, 7, 32, 1),     # other network shapes
+    (40, 13, 0, 64, 2),     # 40 % 16 != 0: the launcher keeps the general form
+])
+def test_field_fwd_uniform_tile_matches_general(mma, n_per_ray, R, extra, width, nhd):
+    """The uniform-tile forward (scalar direction per 16-row tile, branch-free buffer stores;
+    anr_ingp_field_force_fwd(1), the default) is bit-identical to the general form (0)."""
+    from atmonr_amd import _lib
+
+    dev = torch.device("cuda:0")
+    M = R * n_per_ray + extra
+    code = _lib.BF16 if mma == "bf16" else _lib.F16
+    g = torch.Generator(device=dev).manual_seed(5)
+    lib = _lib.load()
+    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, 4, width, nhd, False)
+    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
+    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
+    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
+    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
+    dirs = torch.rand(R + 1, 3, device=dev, generator=g)
+    s = _lib.stream(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", pb, db, code, pp.data_ptr(), pd.data_ptr(),
+              packed.data_ptr(), s)
+    out = {}
+    for mode in (0, 1):
+        prev = lib.anr_ingp_field_force_fwd(mode)
+        try:
+            sigma = torch.full((M + 16,), float("nan"), device=dev)
+            color = torch.full((M + 16, 4), float("nan"), device=dev)
+            _lib.call("anr_ingp_field_fwd", pb, db, code, packed.data_ptr(), enc.data_ptr(), 32,
+                      dirs.data_ptr(), n_per_ray, M, sigma.data_ptr(), color.data_ptr(), 4, s)
+            torch.cuda.synchronize(dev)
+        finally:
+            lib.anr_ingp_field_force_fwd(prev)
+        out[mode] = (sigma, color)
+    for a, b in zip(out[0], out[1]):
+        assert torch.isfinite(a[:M]).all()
+        assert torch.equal(a[:M], b[:M])
+        assert torch.isnan(a[M:]).all() and torch.isnan(b[M:]).all()  # nothing past row M
+
+
 def _field_torch_f32(enc_h, dirs, n_per_ray, pp, pd, width, nhd, nb, h):
     """The fused field in torch f32 on the device with the kernel's 16-bit roundings (h):
     pos 32 -> W -> 16, SH2 | pos_out[1:16] | 1.0 padding, dir 32 -> W (x nhd) -> 16 -> nb."""

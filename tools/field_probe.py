@@ -30,11 +30,14 @@ def main():
     ap.add_argument("--nhd", type=int, default=2)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--bf16", action="store_true", help="bf16 MFMA operands (configs[4])")
+    ap.add_argument("--fwd-mode", type=int, default=1,
+                    help="anr_ingp_field_force_fwd: 1 uniform-tile form (default), 0 general")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     M = args.rays * args.samples
     lib = _lib.load()
+    lib.anr_ingp_field_force_fwd(args.fwd_mode)
     pd_ = _lib.mlp_desc(32, 16, args.width, 1, False)
     dd_ = _lib.mlp_desc(19, 4, args.width, args.nhd, False)
     pdesc, ddesc = ctypes.byref(pd_), ctypes.byref(dd_)
@@ -71,6 +74,9 @@ def main():
     for k, v in timer.summary().items():
         print(f"{k:12s} avg {v['avg_ms']:.4f} ms  ({v['launches']} calls)")
     print("finite:", bool(torch.isfinite(d_enc).all()), bool(torch.isfinite(g_dir).all()))
+    # equal checksums across library builds = the same forward outputs (A/B runs)
+    print(f"checksum sigma {sigma.double().sum().item()!r} color {color.double().sum().item()!r} "
+          f"d_enc {d_enc.double().abs().sum().item()!r}")
     if hasattr(lib, "anr_debug_field_stamps"):  # FIELD_STAMP builds: per-stage cycles
         buf = (ctypes.c_ulonglong * 16)()
         lib.anr_debug_field_stamps(buf)

@@ -1217,9 +1217,22 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       asm volatile("" : "+v"(zoff));
       wbt = wsm + zoff;
     }
+    // The previous tile's raw directions and dL/dsigma, kept live to the end of the tile:
+    // the loop-carried copies of the next tile's prefetched values then sit at the end of
+    // the iteration. Without it they die early (the direction remap is the forward
+    // recompute's first stage) and the compiler copies the prefetch registers right after,
+    // a third into the tile, with an s_waitcnt for the next tile's loads (1 wave/SIMD:
+    // nothing hides it). 0.990 -> 0.967 ms on the bench shape (profiles/r02_field_bwd_keep.log).
+    float keep[8] = {};
     if constexpr (FAST && FULL) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) raw_to_rows(nraw[mt], g, cur[mt]);
+      for (int mt = 0; mt < 2; ++mt) {
+        raw_to_rows(nraw[mt], g, cur[mt]);
+        keep[3 * mt] = nraw[mt].d0;
+        keep[3 * mt + 1] = nraw[mt].d1;
+        keep[3 * mt + 2] = nraw[mt].d2;
+        keep[6 + mt] = nraw[mt].ds;
+      }
       const int64_t tn = tile + 1 < t_full_end ? tile + 1 : tile;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, tn * 32 + mt * 16 + li, g, nraw[mt]);
@@ -1360,6 +1373,9 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         }
       }
     }
+    if constexpr (FAST && FULL)
+      asm volatile("" ::"v"(keep[0]), "v"(keep[1]), "v"(keep[2]), "v"(keep[3]), "v"(keep[4]),
+                   "v"(keep[5]), "v"(keep[6]), "v"(keep[7]));
     // the last dW MFMAs of the tile have written their accumulators before anything
     // (a loop-exit copy) reads them
     agpr_fence();

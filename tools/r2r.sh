@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical (r02): the libanr_ff_{nm2,ld1,ld1nm2} variants were built from experiment
+# macros that were removed after this run (profiles/r02_field_fwd_prefetch_depth.log).
 # Field forward A/B: two 16-sample tiles per step (FIELD_FWD_NM=2) and the dir hidden
 # layer's weights in LDS (FIELD_FWD_LDS_D1=1: 118 VGPRs, 4 waves/SIMD), tools/field_probe.py.
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical (r02): the --bwd-mode probe option and the uniform-tile backward it selected
+# were reverted after this run (profiles/r02_field_bwd_uniform_tile_failed.log).
 # Field backward uniform-tile form (scalar per-half directions): field GPU tests, probe
 # A/B of anr_ingp_field_force_bwd 2 (general rt) vs 1 (uniform-tile rt), one bench run.
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical (r02): the HASH_BWD_STATIC variant was removed after this run
+# (profiles/r02_hash_bwd_static_count_failed.log).
 # Hash-grid backward with a static count of vector-memory instructions per batch
 # (HASH_BWD_STATIC=1: buffer atomics with out-of-range offsets for idle lanes, full
 # batches in their own loop): A/B vs the product library, then the hash GPU tests.

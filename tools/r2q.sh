@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical (r02): the FIELD_FWD_PF variants were removed after this run
+# (profiles/r02_field_fwd_prefetch_depth.log).
 # Field forward prefetch-depth A/B (FIELD_FWD_PF) on the bench shape, then the field GPU
 # tests and one bench run with the product library.
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# Historical (r02): the FIELD_BWD_KEEP experiment macro became the product code after
+# this run (profiles/r02_field_bwd_keep.log).
 # Field backward: keep the previous tile's raw directions (KEEP=1) and d_sigma (KEEP=2)
 # live to the end of the iteration, so the loop-carried copies of the prefetched inputs
 # move to the iteration's end (no mid-tile vmcnt wait). Probe A/B vs the product library,

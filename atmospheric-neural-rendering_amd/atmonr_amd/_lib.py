@@ -250,6 +250,28 @@ _SIGNATURES = {
         c_int32,
         [c_int32, _P, c_int32, c_int32, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P],
     ),
+    "anr_composite_ref16_fwd": (
+        c_int32,
+        [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, _P, _P, _P, _P, _P, _P],
+    ),
+    "anr_composite_ref16_bwd": (
+        c_int32,
+        [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, _P, _P, _P, _P, c_int32,
+         _P, _P],
+    ),
+    "anr_loss_ref16_fwd_bwd": (
+        c_int32, [c_int32, _P, c_int32, _P, _P, c_int64, c_float, _P, _P, _P, _P]),
+    "anr_grad_quantize_f16": (c_int32, [_P, c_int64, c_float, _P]),
+    "anr_ingp_field_bwd_ref16": (
+        c_int32,
+        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
+         c_int64, _P, c_int64, _P, _P, c_float, _P],
+    ),
+    "anr_mlp_bwd_ref16": (
+        c_int32,
+        [POINTER(MlpDesc), _P, _P, c_int32, c_int64, c_int64, _P, c_int32, c_int64, _P,
+         c_int32, c_int64, _P, _P, c_int64, c_float, _P],
+    ),
     "anr_adam_step": (
         c_int32,
         [_P, _P, _P, _P, _P, c_int64, c_float, c_float, c_float, c_float, c_float,

@@ -172,18 +172,28 @@ class IngpFieldFn(torch.autograd.Function):
         d_enc = torch.empty(M, enc.shape[1], device=dev, dtype=torch.float32)
         pdesc, ddesc = ctypes.byref(pipe.pos_mlp.desc), ctypes.byref(pipe.dir_mlp.desc)
         mma = _mma_code(pipe)
-        ws_bytes = _lib.load().anr_ingp_field_bwd_workspace_bytes(pdesc, ddesc, mma, M)
-        ws = torch.empty(max(1, -(-ws_bytes // 4)), device=dev, dtype=torch.float32)
-        if ctx.rows is None:
-            call("anr_ingp_field_bwd", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc.stride(0),
+        ls = getattr(pipe, "loss_scale", None)
+        if ls:
+            # reference numerics: tcnn's loss-scaled f16 backward (anr_ingp_field_bwd_ref16)
+            if ctx.rows is not None:
+                raise _lib.ANRError("reference numerics: no occupancy culling")
+            call("anr_ingp_field_bwd_ref16", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
                  ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color), d_color.stride(0),
-                 ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), ptr(ws), ws_bytes, s,
+                 ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), float(ls), s,
                  tag="field_bwd")
-        else:  # dL/d(sigma, color) are dense; read at the kept samples' rows
-            call("anr_ingp_field_bwd_rows", pdesc, ddesc, mma, ptr(packed), ptr(enc),
-                 enc.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(ctx.rows), ptr(d_sigma),
-                 ptr(d_color), d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos),
-                 ptr(g_dir), ptr(ws), ws_bytes, s, tag="field_bwd")
+        else:
+            ws_bytes = _lib.load().anr_ingp_field_bwd_workspace_bytes(pdesc, ddesc, mma, M)
+            ws = torch.empty(max(1, -(-ws_bytes // 4)), device=dev, dtype=torch.float32)
+            if ctx.rows is None:
+                call("anr_ingp_field_bwd", pdesc, ddesc, mma, ptr(packed), ptr(enc),
+                     enc.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
+                     d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
+                     ptr(ws), ws_bytes, s, tag="field_bwd")
+            else:  # dL/d(sigma, color) are dense; read at the kept samples' rows
+                call("anr_ingp_field_bwd_rows", pdesc, ddesc, mma, ptr(packed), ptr(enc),
+                     enc.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(ctx.rows), ptr(d_sigma),
+                     ptr(d_color), d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos),
+                     ptr(g_dir), ptr(ws), ws_bytes, s, tag="field_bwd")
         _done(direct_p, p_pos, direct_d, p_dir)  # MLP grads final: their all-reduce may start
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")

@@ -78,6 +78,72 @@ class _CompositeFn(torch.autograd.Function):
         return d_z, d_color, d_sigma, d_cs, None, None
 
 
+class _CompositeRef16Fn(torch.autograd.Function):
+    """render_with_surface with the reference's f16 numerics (anr_composite_ref16_*)."""
+
+    @staticmethod
+    def forward(ctx, z, color, sigma, color_surf, z_scale: float, zero_rays):
+        B, N, C = color.shape
+        if sigma.shape[2] != 1:
+            raise ANRError("reference-numerics composite: one density channel (B, N, 1)")
+        dev = color.device
+        color, sigma = color.contiguous(), sigma.contiguous()
+        cs = color_surf.to(color.dtype).contiguous() if color_surf is not None else None
+        zc = z.float().contiguous()
+        f16 = torch.float16
+        cm = torch.empty(B, C, device=dev, dtype=f16)
+        atmo = torch.empty(B, C, device=dev, dtype=f16)
+        surf = torch.empty(B, C, device=dev, dtype=f16) if cs is not None else None
+        weights = torch.empty(B, N, 1, device=dev, dtype=f16)
+        alpha = torch.empty(B, N, 1, device=dev, dtype=f16)
+        call("anr_composite_ref16_fwd", ptr(zc), float(z_scale), ptr(color), ptr(sigma), ptr(cs),
+             dtype_code(color.dtype), B, N, C, ptr(cm), ptr(atmo), ptr(surf), ptr(weights),
+             ptr(alpha), _lib.stream(dev), tag="composite_fwd")
+        ctx.save_for_backward(zc, color, sigma, cs)
+        ctx.set_materialize_grads(False)
+        ctx.z_scale = float(z_scale)
+        ctx.zero_rays = zero_rays
+        if cs is None:
+            return cm, alpha, weights
+        return cm, alpha, weights, atmo, surf
+
+    @staticmethod
+    def backward(ctx, g_cm, *unused):
+        zc, color, sigma, cs = ctx.saved_tensors
+        if any(g is not None for g in unused):
+            raise ANRError("reference-numerics composite: gradients flow through color_map "
+                           "only (as in the reference's loss)")
+        B, N, C = color.shape
+        dev = color.device
+        if g_cm is None:
+            g_cm = torch.zeros(B, C, device=dev, dtype=torch.float16)
+        g_cm = g_cm.to(torch.float16).contiguous()
+        d_color = torch.empty_like(color)
+        d_sigma = torch.empty_like(sigma)
+        d_cs = torch.empty_like(cs) if cs is not None and ctx.needs_input_grad[3] else None
+        call("anr_composite_ref16_bwd", ptr(zc), ctx.z_scale, ptr(color), ptr(sigma), ptr(cs),
+             dtype_code(color.dtype), B, N, C, ptr(g_cm), ptr(d_color), ptr(d_sigma), ptr(d_cs),
+             dtype_code(color.dtype), ptr(ctx.zero_rays), _lib.stream(dev),
+             tag="composite_bwd")
+        return None, d_color, d_sigma, d_cs, None, None
+
+
+def render_with_surface_ref16(z_vals, color, sigma, color_surf, z_scale: float = 1.0,
+                              zero_rays: torch.Tensor | None = None):
+    """graphics_utils.py:52-77 with the reference's Instant-NGP numerics: z cast to f16
+    (after the f32 ``z_vals * z_scale``), every op rounded to f16, torch's CUDA
+    accumulation (f16 cumprod / cumsum, f32 sum / prod), and torch's f16 autograd as the
+    backward (csrc/ref16.hip; restated in oracle/ref_f16.py). color / sigma / color_surf
+    may be f32 (rounded to f16 on load, as a tcnn f16 output would be). Returns f16
+    (color_map, alpha, weights, atmo, surf). ``zero_rays`` (int32 device tensor, optional)
+    counts rays whose alpha rounded to exactly 1 in f16 (torch's zero-input backward
+    branch, not reproduced: those rays get zero gradients)."""
+    _check(z_vals, color, sigma)
+    if zero_rays is None:
+        zero_rays = torch.zeros(1, dtype=torch.int32, device=color.device)
+    return _CompositeRef16Fn.apply(z_vals, color, sigma, color_surf, z_scale, zero_rays)
+
+
 def _check(z_vals, color, sigma):
     if not (z_vals.dim() == 2 and color.dim() == 3 and sigma.dim() == 3):
         raise ANRError("render: expected z (B,N), color (B,N,C), sigma (B,N,S)")

@@ -38,6 +38,39 @@ class _IndexedLossFn(torch.autograd.Function):
         return (grad * dloss.to(grad.dtype)), None, None, None, None
 
 
+class _IndexedLossRef16Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, color_map, irgb_idx, gt, max_i: float, code: int):
+        B, C = color_map.shape
+        dev = color_map.device
+        cm = color_map.to(torch.float16).contiguous()
+        idx = irgb_idx.to(torch.int64).contiguous()
+        g = gt.float().contiguous()
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        grad = torch.empty_like(cm) if ctx.needs_input_grad[0] else None
+        ws = torch.empty(int(_lib.load().anr_loss_workspace_bytes(B)) // 4 + 1, device=dev)
+        call("anr_loss_ref16_fwd_bwd", code, ptr(cm), C, ptr(idx), ptr(g), B, float(max_i),
+             ptr(loss), ptr(grad), ptr(ws), _lib.stream(dev), tag="loss")
+        ctx.save_for_backward(grad)
+        return loss.to(torch.float16)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (grad,) = ctx.saved_tensors
+        if grad is None:
+            return None, None, None, None, None
+        return (grad * dloss.to(grad.dtype)), None, None, None, None
+
+
+def indexed_loss_ref16(name: str, color_map: torch.Tensor, irgb_idx: torch.Tensor,
+                       gt: torch.Tensor, max_i: float) -> torch.Tensor:
+    """:func:`indexed_loss` with the reference's f16 numerics (instant_ngp.py:259-263 on
+    an f16 colour map: the target cast to f16, every loss op and its autograd in f16;
+    csrc/ref16.hip, restated in oracle/ref_f16.py). Returns an f16 scalar."""
+    return _IndexedLossRef16Fn.apply(color_map, irgb_idx, gt, float(max_i),
+                                     LOSS_CODES[name.lower()])
+
+
 def indexed_loss(name: str, color_map: torch.Tensor, irgb_idx: torch.Tensor, gt: torch.Tensor,
                  max_i: float) -> torch.Tensor:
     """loss_fn(take_along_dim(color_map, irgb_idx[:, None], 1)[:, 0], gt, max_i)."""

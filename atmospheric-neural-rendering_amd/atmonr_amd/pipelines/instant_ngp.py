@@ -13,6 +13,17 @@ Two execution paths, identical semantics:
 * ``fused=False``: the reference's op-by-op graph (sample_uniform_bins, the point
   preprocessor, the (p+1)/2 remap, tcnn-style modules with f16 outputs) on the same
   kernels — used to check that the fused path changes nothing but speed.
+
+Two numerics (``numerics=`` or the config key ``"numerics"``):
+
+* ``"build"`` (default): f16 tables / weights / activations as tcnn, but the composite,
+  the loss and every inter-kernel gradient in f32 (no f16 underflow in the backward).
+* ``"reference"``: the reference's own f16 arithmetic wherever it differs — the composite
+  and the loss as chains of f16 torch ops with torch's f16 autograd (graphics_utils.py:
+  28-76, instant_ngp.py:259-263; csrc/ref16.hip), tinycudann's loss-scaled (x128) f16
+  module backward with f16 gradients at the module boundaries, and tcnn's f16 parameter
+  gradients (tinycudann/modules.py). Opt-in, for PSNR parity with the reference; f16
+  networks, fused field, no occupancy culling.
 """
 
 from __future__ import annotations
@@ -27,8 +38,8 @@ from torch.optim import Optimizer
 
 from .. import _lib
 from ..field import IngpFieldFn, field_density, field_fused
-from ..graphics_utils import render_with_surface
-from ..losses import LOSSES, indexed_loss
+from ..graphics_utils import render_with_surface, render_with_surface_ref16
+from ..losses import LOSSES, indexed_loss, indexed_loss_ref16
 from ..occupancy import OccupancyGrid, pipeline_density
 from ..optim import FusedAdam
 from ..samplers import preprocess_points, sample_and_preprocess, sample_uniform_bins
@@ -42,12 +53,17 @@ class InstantNGPPipeline(Pipeline):
 
     def __init__(self, config: dict, dataset: Any, dtype: torch.dtype = torch.float16,
                  fused: bool = True, seed: int = 1337, occupancy=None,
-                 mlp_dtype: torch.dtype | None = None) -> None:
+                 mlp_dtype: torch.dtype | None = None, numerics: str | None = None) -> None:
         """``dtype``: tcnn compute precision of every module (f16 as the reference, or f32).
         ``mlp_dtype=torch.bfloat16`` (BASELINE configs[4], beyond the reference): the
         per-sample pos / dir MLPs run bf16 MFMA over the f16 hash features (fused field
-        only); the per-ray surface network keeps ``dtype``."""
+        only); the per-ray surface network keeps ``dtype``. ``numerics``: "build" or
+        "reference" (module docstring)."""
         super().__init__(config, dataset)
+        numerics = numerics or self.config.get("numerics", "build")
+        if numerics not in ("build", "reference"):
+            raise ValueError(f"numerics {numerics!r}: 'build' or 'reference'")
+        self.numerics = numerics
         self.num_density_outputs = 1
         if self.config["multi_band_extinction"]:
             self.num_density_outputs = self.config["num_bands"]
@@ -61,10 +77,19 @@ class InstantNGPPipeline(Pipeline):
         if mlp_dtype == torch.bfloat16 and (dtype != torch.float16 or not fused):
             raise ValueError("bf16 field MLPs need f16 hash features and the fused path")
         self.mlp_dtype = mlp_dtype
+        # tinycudann's loss scale for f16 modules (reference numerics only)
+        self.loss_scale = 128.0 if numerics == "reference" else None
+        if numerics == "reference" and not (fused and dtype == torch.float16 and
+                                            mlp_dtype == torch.float16 and occupancy is None):
+            raise ValueError("numerics='reference' runs the fused f16 field (f16 modules, "
+                             "no occupancy culling)")
+        self._zero_rays = None
         self.surface_stream = os.environ.get("ANR_SURFACE_STREAM", "1") != "0"
         ingp = self.config["instant_ngp"]
         nb = self.config["num_bands"]
-        fdt = torch.float32 if fused else None  # fused path keeps activations/grads in f32
+        # the fused path keeps activations / gradients in f32 (build numerics); tcnn's f16
+        # outputs in reference numerics
+        fdt = torch.float32 if fused and numerics == "build" else None
         self.pos_encoder = Encoding(3, ingp["encoding"], seed=seed, dtype=dtype)
         self.pos_mlp = Network(self.pos_encoder.n_output_dims, 16, ingp["network"],
                                seed=seed + 1, dtype=mlp_dtype)
@@ -76,6 +101,7 @@ class InstantNGPPipeline(Pipeline):
                                      dtype=dtype, output_dtype=fdt)
         self.surf_mlp = Network(self.surf_encoder.n_output_dims, nb, ingp["surface_network"],
                                 seed=seed + 5, dtype=dtype, output_dtype=fdt)
+        self.surf_mlp.loss_scale = self.loss_scale
         d = self.dir_mlp.desc
         self._dir_desc_relu = _lib.mlp_desc(d.n_input, d.n_output, d.width, d.n_hidden_layers,
                                             True)
@@ -90,7 +116,7 @@ class InstantNGPPipeline(Pipeline):
         # occupancy-grid culling (beyond the reference, atmonr_amd.occupancy): off unless
         # passed in or configured; the uniform sampler stays the parity default
         occ_cfg = self.config.get("occupancy_grid")
-        if occupancy is None and occ_cfg:
+        if occupancy is None and occ_cfg and numerics == "build":
             occupancy = OccupancyGrid.from_config(occ_cfg, self.alt_compress,
                                                   getattr(dataset, "device", None))
         self.occupancy = occupancy
@@ -186,8 +212,18 @@ class InstantNGPPipeline(Pipeline):
         color = color.view(B, N, -1)
         sigma = sigma.view(B, N, 1)
         color_surf = surf_branch()
-        color_map, _, weights, atmo, surf = render_with_surface(
-            z_vals, color, sigma, color_surf, z_scale=self.scale / 1000)
+        if self.numerics == "reference":
+            if self._zero_rays is None:
+                self._zero_rays = torch.zeros(1, dtype=torch.int32, device=color.device)
+            color_map, _, weights, atmo, surf = render_with_surface_ref16(
+                z_vals, color, sigma, color_surf, z_scale=self.scale / 1000,
+                zero_rays=self._zero_rays)
+            if color_map.requires_grad:
+                color_map = _TcnnGradsAtBackwardEnd.apply(color_map, self)
+            color, sigma = color.half(), sigma.half()  # tcnn's f16 outputs in the results
+        else:
+            color_map, _, weights, atmo, surf = render_with_surface(
+                z_vals, color, sigma, color_surf, z_scale=self.scale / 1000)
         return {
             "color_fine": color[:, :-1],
             "color_surf": color_surf,
@@ -250,6 +286,9 @@ class InstantNGPPipeline(Pipeline):
     def compute_loss(self, ray_batch: Mapping[str, torch.Tensor],
                      results: dict[str, torch.Tensor]) -> torch.Tensor:
         """loss_fn(take_along_dim(color_map, irgb_idx), rad, max_i) (instant_ngp.py:249-263)."""
+        if self.numerics == "reference":
+            return indexed_loss_ref16(self.loss_name, results["color_map_fine"],
+                                      ray_batch["irgb_idx"], ray_batch["rad"], self.max_i)
         return indexed_loss(self.loss_name, results["color_map_fine"], ray_batch["irgb_idx"],
                             ray_batch["rad"], self.max_i)
 
@@ -270,3 +309,35 @@ class InstantNGPPipeline(Pipeline):
         self.training = False
         for m in self.modules():
             m.eval()
+
+
+class _TcnnGradsAtBackwardEnd(torch.autograd.Function):
+    """Identity on the colour map (reference numerics). Its backward queues an
+    end-of-backward callback that turns every module's accumulated f32 parameter gradient
+    into the value tinycudann hands to torch: the module's f16 gradient at loss scale 128,
+    divided by 128 in f16 (tinycudann/modules.py; anr_grad_quantize_f16). The callback
+    runs once the whole backward has been enqueued; it first joins the surface branch's
+    side stream, whose kernels write that branch's gradients."""
+
+    @staticmethod
+    def forward(ctx, x, pipe):
+        ctx.pipe = pipe
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        pipe = ctx.pipe
+        dev = g.device
+
+        def quantize():
+            main = torch.cuda.current_stream(dev)
+            main.wait_stream(_lib.side_stream(dev))
+            for m in pipe.modules():
+                p = m.params
+                if p.numel() and p.grad is not None:
+                    if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
+                        raise _lib.ANRError("reference numerics: f32 contiguous grads only")
+                    _lib.call("anr_grad_quantize_f16", _lib.ptr(p.grad), p.grad.numel(),
+                              float(pipe.loss_scale), _lib.stream(dev), tag="grad_quantize")
+        torch.autograd.Variable._execution_engine.queue_callback(quantize)
+        return g, None

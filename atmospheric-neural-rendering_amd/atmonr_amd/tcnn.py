@@ -269,11 +269,18 @@ class _NetworkFn(torch.autograd.Function):
         ws_bytes = net.bwd_workspace_bytes(x.shape[0])
         ws = (torch.empty(ws_bytes // 4, device=x.device, dtype=torch.float32)
               if ws_bytes else None)
-        call("anr_mlp_bwd_ws", ctypes.byref(net.desc), prec, ptr(p), ptr(x),
-             dtype_code(x.dtype), x.stride(0), x.shape[0], ptr(dout), dtype_code(dout.dtype),
-             dout.stride(0), ptr(din), dtype_code(x.dtype),
-             x.stride(0) if din is not None else 0, ptr(dparams), ptr(ws), ws_bytes,
-             _lib.stream(x.device))
+        if net.loss_scale:  # tcnn's loss-scaled f16 backward (reference numerics)
+            call("anr_mlp_bwd_ref16", ctypes.byref(net.desc), ptr(p), ptr(x),
+                 dtype_code(x.dtype), x.stride(0), x.shape[0], ptr(dout),
+                 dtype_code(dout.dtype), dout.stride(0), ptr(din), dtype_code(x.dtype),
+                 x.stride(0) if din is not None else 0, ptr(dparams), ptr(ws), ws_bytes,
+                 float(net.loss_scale), _lib.stream(x.device))
+        else:
+            call("anr_mlp_bwd_ws", ctypes.byref(net.desc), prec, ptr(p), ptr(x),
+                 dtype_code(x.dtype), x.stride(0), x.shape[0], ptr(dout),
+                 dtype_code(dout.dtype), dout.stride(0), ptr(din), dtype_code(x.dtype),
+                 x.stride(0) if din is not None else 0, ptr(dparams), ptr(ws), ws_bytes,
+                 _lib.stream(x.device))
         if direct:
             _lib.grad_done(net.params)
         return din, None if direct else dparams, None
@@ -311,6 +318,9 @@ class Network(nn.Module):
         self.network_config = network_config
         self.dtype = torch.float16 if dtype is None else dtype
         self.output_dtype = self.dtype if output_dtype is None else output_dtype
+        # None: the kernels' own per-wavefront f16 gradient scaling; a number (tcnn: 128):
+        # tinycudann's fixed loss scale and its f16 input gradient (reference numerics)
+        self.loss_scale: float | None = None
         self.width = int(cfg.get("n_neurons", 64))
         self.n_hidden_layers = int(cfg.get("n_hidden_layers", 2))
         self.desc = _lib.mlp_desc(n_input_dims, n_output_dims, self.width, self.n_hidden_layers,

@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(CompArgs a) {
           if (a.d_weights) q[s] += ldv(static_cast<const T*>(a.d_weights), o);
           const float sg = ldv(sig, i * S + s);
           const float al = alpha_of(sg * dl);
-          const float e = 1.0f - al;
+          const float e = expf(-(sg * dl));  // d alpha / dx, accurate where alpha -> 1
           const float t = (1.0f - al) + 1e-10f;
           const float Ti = T_in[s] * Tloc[i * S + s];
           const float Pi = P_in[s] * Ploc[i * S + s];
@@ -566,7 +566,8 @@ __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
       const int o = j * S + s;
       if (a.d_weights && j < nvalid) qq[s] += ldv(static_cast<const T*>(a.d_weights), (b * N + i0 + j) * S + s);
       const float ao = alpha_of(sg[o] * dl[j]);
-      const float ee = 1.0f - ao;
+      // d alpha / dx = exp(-x) on its own: 1 - alpha cancels once alpha nears 1 (x > ~8)
+      const float ee = expf(-(sg[o] * dl[j]));
       e[o] = ee;
       al[o] = j < nvalid ? ao : 0.0f;
       q[o] = j < nvalid ? qq[s] : 0.0f;

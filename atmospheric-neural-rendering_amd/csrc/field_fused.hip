@@ -268,6 +268,9 @@ struct Args {
   // occupancy-compacted samples (nullable): row r of enc / d_enc is sample rows[r] of the
   // dense (ray-major) arrays sigma, color, d_sigma, d_color; its ray is rows[r] / n_per_ray
   const int32_t* rows;
+  // > 0: reference numerics (tcnn's loss-scaled f16 backward, anr_ingp_field_bwd_ref16):
+  // fixed gradient scale, f16 module-boundary gradients; 0: per-wavefront dynamic scale
+  float loss_scale;
 };
 
 // ROWS is a compile-time choice: a run-time test on a.rows in the prefetch paths put a
@@ -1155,9 +1158,17 @@ __device__ __forceinline__ h4 tr_b(h8 x, h8 sel) {
   return to_h4<BF>(mma32<BF>(x, sel, f4{0.0f, 0.0f, 0.0f, 0.0f}));
 }
 
-template <int W, int NHD, bool FAST, bool ROWS, bool BF>
+// REF (reference numerics, f16 only): the gradient scale is tcnn's fixed loss scale
+// (a.loss_scale = 128) instead of the per-wavefront power of two, the ReLU masks test the
+// f16-rounded outputs, and the gradients that cross tinycudann module boundaries in the
+// reference are rounded as they are there: dL/dpos_out[1:16] comes back from dir_mlp /
+// dir_encoder as f16(f16(g_scaled) / 128) (a subnormal-flushing f16 division) and is
+// rescaled for pos_mlp, and dL/denc is written as f16(f16(g_scaled) / 128)
+// (tinycudann/modules.py: input_grad / loss_scale, cast to the f16 input's dtype).
+template <int W, int NHD, bool FAST, bool ROWS, bool BF, bool REF = false>
 __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64_t tpw,
                                                      const float* wmax) {
+  static_assert(!(REF && BF), "reference numerics are f16");
   using N = Net<W, NHD>;
   constexpr int NT = N::NT, KB = N::KB;
   __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
@@ -1191,7 +1202,10 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     for (int i = 0; i < NT * NT; ++i) dD1[i] = z4;
   }
   float s = 1.0f, inv_s = 1.0f;
-  if constexpr (!BF) {
+  if constexpr (REF) {
+    s = a.loss_scale;
+    inv_s = 1.0f / a.loss_scale;
+  } else if constexpr (!BF) {
     const float gm = t_begin < t_end ? wmax[w_id] : 0.0f;
     if (gm > 0.0f) {
       int e = static_cast<int>(floorf(log2f(target / gm)));
@@ -1200,6 +1214,8 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       inv_s = ldexpf(1.0f, -e);
     }
   }
+  // f32 -> f16 -> f32 (the reference's f16 tensors between modules)
+  auto r16 = [](float v) { return static_cast<float>(static_cast<_Float16>(v)); };
 
   Rows cur[2];
   RawRows nraw[2];
@@ -1254,10 +1270,11 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       tile_forward<W, NHD, 2, BF>(fwl, cur, valid, g, t, NoSink{});
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        dens[mt] = t[mt].po[0] > 0.0f;
+        dens[mt] = (REF ? r16(t[mt].po[0]) : t[mt].po[0]) > 0.0f;
         f4 gv;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) gv[i] = t[mt].col[i] > 0.0f ? cur[mt].dc[i] * s : 0.0f;
+        for (int i = 0; i < 4; ++i)
+          gv[i] = (REF ? r16(t[mt].col[i]) : t[mt].col[i]) > 0.0f ? cur[mt].dc[i] * s : 0.0f;
         gc[mt] = to_h4<BF>(gv);
       }
     }
@@ -1325,6 +1342,10 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       }
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
+        if constexpr (REF) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[mt][i] = r16(r16(r16(acc[mt][i]) * inv_s) * s);
+        }
         // pos_out[:, 0] is the density: its gradient is dL/dsigma through the ReLU
         const float dsv = dens[mt] ? cur[mt].ds * s : 0.0f;
         acc[mt][0] = g == 0 ? dsv : acc[mt][0];
@@ -1367,7 +1388,11 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         for (int mt = 0; mt < 2; ++mt) {
           const int64_t row = tile * 32 + mt * 16 + li;
           if (full || row < a.M) {
-            const f4 v = acc[mt] * inv_s;
+            f4 v = acc[mt] * inv_s;
+            if constexpr (REF) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) v[i] = r16(r16(acc[mt][i]) * inv_s);
+            }
             *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
           }
         }
@@ -1509,6 +1534,22 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
     return 0;
   }
   const bool fast = a.n_out == 4 && (a.d_color_stride & 3) == 0 && a.d_sigma != nullptr;
+  if (a.loss_scale > 0.0f) {  // reference numerics: the register-transposed kernel, REF
+    if constexpr (BF) {
+      return 1;
+    } else {
+      if (a.rows) return 1;
+      const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast, 1);
+      const dim3 grid(static_cast<unsigned>(gm.blocks)), block(64 * waves);
+      if (fast)
+        hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, true, false, false, true>), grid, block, 0, st, a,
+                           0.0f, gm.tpw, nullptr);
+      else
+        hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, false, false, false, true>), grid, block, 0, st,
+                           a, 0.0f, gm.tpw, nullptr);
+      return 0;
+    }
+  }
   const int mode = g_bwd_mode;
   const size_t lds = (static_cast<size_t>(N::n_packed) + (mode == 1 ? 0 : waves * N::wave_lds)) * 2;
   if (lds > 160 * 1024) return 1;
@@ -1694,9 +1735,11 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
                      int64_t n_per_ray, int64_t M, const int32_t* rows, const float* d_sigma,
                      const float* d_color, int64_t d_color_stride, float* d_enc,
                      int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
-                     int64_t workspace_bytes, anr_stream_t stream) {
+                     int64_t workspace_bytes, anr_stream_t stream, float loss_scale = 0.0f) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_bwd: unsupported pos/dir MLP pair");
+  ANR_CHECK_ARG(loss_scale == 0.0f || (loss_scale > 0.0f && mma_dtype == ANR_F16 && rows == nullptr),
+                "anr_ingp_field_bwd: reference numerics need f16 MMA and dense rows");
   ANR_CHECK_ARG(mma_ok(mma_dtype), "anr_ingp_field_bwd: mma_dtype must be ANR_F16 or ANR_BF16");
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_bwd: bad M");
   if (M == 0) return ANR_OK;
@@ -1726,6 +1769,7 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   a.g_pos = g_pos;
   a.g_dir = g_dir;
   a.rows = rows;
+  a.loss_scale = loss_scale;
   const int rc = dispatch(v, mma_dtype == ANR_BF16, 2, a, static_cast<float*>(workspace),
                           workspace_bytes, reinterpret_cast<hipStream_t>(stream));
   ANR_CHECK_ARG(rc != 2,
@@ -1755,6 +1799,19 @@ extern "C" int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* d
   return field_bwd(pos, dir, mma_dtype, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
                    d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir,
                    workspace, workspace_bytes, stream);
+}
+
+extern "C" int anr_ingp_field_bwd_ref16(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                        const void* packed, const void* enc, int64_t enc_stride,
+                                        const float* dirs, int64_t n_per_ray, int64_t M,
+                                        const float* d_sigma, const float* d_color,
+                                        int64_t d_color_stride, float* d_enc,
+                                        int64_t d_enc_stride, float* g_pos, float* g_dir,
+                                        float loss_scale, anr_stream_t stream) {
+  ANR_CHECK_ARG(loss_scale > 0.0f, "anr_ingp_field_bwd_ref16: loss_scale must be > 0");
+  return field_bwd(pos, dir, ANR_F16, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
+                   d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, nullptr,
+                   0, stream, loss_scale);
 }
 
 extern "C" int anr_ingp_field_fwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,

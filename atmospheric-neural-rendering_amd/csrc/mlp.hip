@@ -406,7 +406,7 @@ int mlp_fused_try(const anr_mlp_desc* d, int32_t precision, bool bwd, const void
                   const void* in, int32_t in_dt, int64_t in_stride, int64_t M,
                   const void* dout, int32_t dout_dt, int64_t dout_stride, void* out,
                   int32_t out_dt, int64_t out_stride, float* dparams, hipStream_t st,
-                  float* slab = nullptr, int64_t slab_floats = 0);
+                  float* slab = nullptr, int64_t slab_floats = 0, float loss_scale = 0.0f);
 bool mlp_fused_has(const anr_mlp_desc* d);
 
 // ANR_MLP_GENERIC=1 (or anr_mlp_force_generic) forces the generic kernels.
@@ -494,10 +494,13 @@ static int mlp_bwd_impl(const anr_mlp_desc* d, int32_t precision, const void* pa
                         const void* in, int32_t in_dtype, int64_t in_stride, int64_t M,
                         const void* dout, int32_t dout_dtype, int64_t dout_stride, void* din,
                         int32_t din_dtype, int64_t din_stride, float* dparams,
-                        void* workspace, int64_t workspace_bytes, anr_stream_t stream) {
+                        void* workspace, int64_t workspace_bytes, anr_stream_t stream,
+                        float loss_scale = 0.0f) {
   using namespace anr;
   if (int rc = check_desc(d)) return rc;
   if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(loss_scale == 0.0f || (loss_scale > 0.0f && precision == ANR_F16),
+                "anr_mlp_bwd: reference numerics (loss_scale) need f16");
   ANR_CHECK_ARG(params && in && dout && dparams, "anr_mlp_bwd: null argument");
   ANR_CHECK_ARG(precision == ANR_F16 || precision == ANR_F32, "anr_mlp_bwd: bad precision");
   ANR_CHECK_ARG(M >= 0 && in_stride >= d->n_input && dout_stride >= d->n_output &&
@@ -508,10 +511,13 @@ static int mlp_bwd_impl(const anr_mlp_desc* d, int32_t precision, const void* pa
       mlp_fused_try(d, precision, true, params, in, in_dtype, in_stride, M, dout, dout_dtype,
                     dout_stride, din, din_dtype, din_stride, dparams, as_stream(stream),
                     M <= kSlabMaxRows ? static_cast<float*>(workspace) : nullptr,
-                    workspace_bytes / static_cast<int64_t>(sizeof(float))) == 0) {
+                    workspace_bytes / static_cast<int64_t>(sizeof(float)), loss_scale) == 0) {
     ANR_CHECK_LAUNCH("anr_mlp_bwd(fused)");
     return ANR_OK;
   }
+  ANR_CHECK_ARG(loss_scale == 0.0f,
+                "anr_mlp_bwd_ref16: no specialised kernel for this shape (reference numerics "
+                "run on the fused MLP kernels only)");
   MlpArgs a = base_args(d, M);
   a.params = params;
   a.in = in;
@@ -573,4 +579,16 @@ extern "C" int anr_mlp_bwd_ws(const anr_mlp_desc* d, int32_t precision, const vo
   return mlp_bwd_impl(d, precision, params, in, in_dtype, in_stride, M, dout, dout_dtype,
                       dout_stride, din, din_dtype, din_stride, dparams, workspace,
                       workspace_bytes, stream);
+}
+
+extern "C" int anr_mlp_bwd_ref16(const anr_mlp_desc* d, const void* params, const void* in,
+                                 int32_t in_dtype, int64_t in_stride, int64_t M,
+                                 const void* dout, int32_t dout_dtype, int64_t dout_stride,
+                                 void* din, int32_t din_dtype, int64_t din_stride,
+                                 float* dparams, void* workspace, int64_t workspace_bytes,
+                                 float loss_scale, anr_stream_t stream) {
+  ANR_CHECK_ARG(loss_scale > 0.0f, "anr_mlp_bwd_ref16: loss_scale must be > 0");
+  return mlp_bwd_impl(d, ANR_F16, params, in, in_dtype, in_stride, M, dout, dout_dtype,
+                      dout_stride, din, din_dtype, din_stride, dparams, workspace,
+                      workspace_bytes, stream, loss_scale);
 }

@@ -122,6 +122,9 @@ struct Args {
   // dparams (small batches: the atomics would pile onto the same few KB)
   float* slab;
   int64_t slab_floats;
+  // > 0 (f16, MODE 0): reference numerics (anr_mlp_bwd_ref16): tcnn's fixed loss scale
+  // instead of the per-wavefront one, and dL/dinput written as f16(f16(g_scaled) / scale)
+  float loss_scale;
 };
 
 // dparams[p] += sum over the nw slab rows of slab[w * n + p]. Block = 64 params x 16 row
@@ -406,7 +409,11 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
   // f16: one power-of-two gradient scale per wavefront (max |dL/dout| over all its rows
   // -> 256), so dW accumulates directly in the MFMA accumulators and is unscaled once.
   float s = 1.0f, inv_s = 1.0f;
-  if constexpr (half) {
+  const bool ref = half && a.loss_scale > 0.0f;
+  if (ref) {
+    s = a.loss_scale;
+    inv_s = 1.0f / a.loss_scale;
+  } else if constexpr (half) {
     float gmax = 0.0f;
     for (int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave; tile < n_tiles;
          tile += static_cast<int64_t>(gridDim.x) * waves) {
@@ -539,14 +546,25 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a) {
             const int64_t row = r0 + (lane & 15);
             const int c0 = nt * 16 + 4 * (lane >> 4);
             if (row < a.M) {
+              if (ref) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                  acc[i] = static_cast<float>(static_cast<_Float16>(acc[i]));
+              }
               if (a.out_dt == ANR_F32 && c0 + 3 < a.n_in && (a.out_stride % 4) == 0) {
                 f4 v = {acc[0] * inv_s, acc[1] * inv_s, acc[2] * inv_s, acc[3] * inv_s};
+                if (ref) {
+#pragma unroll
+                  for (int i = 0; i < 4; ++i) v[i] = static_cast<float>(static_cast<_Float16>(v[i]));
+                }
                 *reinterpret_cast<f4*>(static_cast<float*>(a.out) + row * a.out_stride + c0) = v;
               } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                   if (c0 + i < a.n_in)
-                    store_dyn(a.out, a.out_dt, row * a.out_stride + c0 + i, acc[i] * inv_s);
+                    store_dyn(a.out, a.out_dt, row * a.out_stride + c0 + i,
+                              ref ? static_cast<float>(static_cast<_Float16>(acc[i] * inv_s))
+                                  : acc[i] * inv_s);
               }
             }
           }
@@ -680,8 +698,9 @@ int mlp_fused_try(const anr_mlp_desc* d, int32_t precision, bool bwd, const void
                   const void* in, int32_t in_dt, int64_t in_stride, int64_t M,
                   const void* dout, int32_t dout_dt, int64_t dout_stride, void* out,
                   int32_t out_dt, int64_t out_stride, float* dparams, hipStream_t st,
-                  float* slab, int64_t slab_floats) {
+                  float* slab, int64_t slab_floats, float loss_scale) {
   fused::Args a{};
+  a.loss_scale = loss_scale;
   a.slab = slab;
   a.slab_floats = slab_floats;
   a.n_in = d->n_input;

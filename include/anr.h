@@ -417,6 +417,65 @@ int anr_loss_fwd_bwd(int32_t loss_type, const void* color_map, int32_t pred_dtyp
                      void* workspace, anr_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
+ * Reference numerics (csrc/ref16.hip; opt-in, InstantNGPPipeline(numerics="reference")).
+ * The reference's Instant-NGP composite and loss run as chains of torch f16 ops on f16
+ * tinycudann outputs (graphics_utils.py:28-76, instant_ngp.py:259-263, losses.py:5-33),
+ * and tcnn's backward is loss-scaled f16 (tinycudann/modules.py, loss scale 128). These
+ * entry points reproduce those roundings op by op (oracle/ref_f16.py is the restatement;
+ * torch's CUDA accumulation: f16 accumulator in cumprod / cumsum, f32 in sum / prod).
+ * One thread per ray; a parity mode, not the performance path.
+ * ------------------------------------------------------------------------------------
+ * Forward: z (B,N) f32 times z_scale in f32 then rounded to f16; color (B,N,C), sigma
+ * (B,N,1), color_surf (B,C) (nullable) in in_dtype, rounded to f16 on load. Outputs f16:
+ * color_map (B,C) [required], color_map_atmo, color_map_surf (B,C), weights, alpha
+ * (B,N,1) (nullable). Replaces render_with_surface (graphics_utils.py:52-77) at
+ * instant_ngp.py:187-192 in that mode. */
+int anr_composite_ref16_fwd(const float* z, float z_scale, const void* color,
+                            const void* sigma, const void* color_surf, int32_t in_dtype,
+                            int64_t B, int32_t N, int32_t C, void* color_map,
+                            void* color_map_atmo, void* color_map_surf, void* weights,
+                            void* alpha, anr_stream_t stream);
+/* Backward from dL/dcolor_map (B,C) f16 (torch's f16 autograd of the forward).
+ * d_color (B,N,C), d_sigma (B,N,1) [required; also scratch for the cumprod outputs] and
+ * d_color_surf (B,C) (nullable) in out_dtype, holding f16 values. zero_rays: one int32
+ * (device), incremented per ray in which alpha rounded to exactly 1 (torch's zero-input
+ * backward branches, not reproduced: that ray's gradients are 0). */
+int anr_composite_ref16_bwd(const float* z, float z_scale, const void* color,
+                            const void* sigma, const void* color_surf, int32_t in_dtype,
+                            int64_t B, int32_t N, int32_t C, const void* d_color_map,
+                            void* d_color, void* d_sigma, void* d_color_surf,
+                            int32_t out_dtype, int32_t* zero_rays, anr_stream_t stream);
+/* Loss in f16 ops: color_map (B,C) f16, gt (B,) f32 (cast to f16 as instant_ngp.py:262),
+ * loss_out: 1 f32 holding the f16 loss value, grad_out (B,C) f16 (nullable),
+ * workspace >= anr_loss_workspace_bytes(B). */
+int anr_loss_ref16_fwd_bwd(int32_t loss_type, const void* color_map, int32_t C,
+                           const int64_t* irgb_idx, const float* gt, int64_t B, float max_i,
+                           float* loss_out, void* grad_out, void* workspace,
+                           anr_stream_t stream);
+/* tcnn's parameter gradient of an f16 module at loss scale s: g <- f16(f16(g*s)/s), in
+ * place over n f32 values (the value tinycudann/modules.py hands to torch). */
+int anr_grad_quantize_f16(float* grad, int64_t n, float loss_scale, anr_stream_t stream);
+/* The fused field backward (anr_ingp_field_bwd) with tcnn's backward semantics: fixed
+ * f16 gradient scale loss_scale (128), ReLU masks on the f16 outputs, and the
+ * module-boundary gradients of the reference (dir_mlp -> dir_encoder -> pos_out, pos_mlp
+ * -> pos_encoder) rounded as f16(f16(g_scaled)/loss_scale). f16 networks, dense rows; no
+ * workspace. */
+int anr_ingp_field_bwd_ref16(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                             const void* packed, const void* enc, int64_t enc_stride,
+                             const float* dirs, int64_t n_per_ray, int64_t M,
+                             const float* d_sigma, const float* d_color,
+                             int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
+                             float* g_pos, float* g_dir, float loss_scale,
+                             anr_stream_t stream);
+/* anr_mlp_bwd_ws in f16 with tcnn's fixed loss scale: dL/dinput written as
+ * f16(f16(g_scaled)/loss_scale). Specialised (fused) MLP shapes only. */
+int anr_mlp_bwd_ref16(const anr_mlp_desc* d, const void* params, const void* in,
+                      int32_t in_dtype, int64_t in_stride, int64_t M, const void* dout,
+                      int32_t dout_dtype, int64_t dout_stride, void* din, int32_t din_dtype,
+                      int64_t din_stride, float* dparams, void* workspace,
+                      int64_t workspace_bytes, float loss_scale, anr_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
  * K10: fused AdamW (torch.optim.AdamW, instant_ngp.py:120-126; Adam nerf.py:70 is
  * weight_decay = 0, decoupled = 0) over one flat f32 parameter buffer.
  * ------------------------------------------------------------------------------------

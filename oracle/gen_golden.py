@@ -187,6 +187,74 @@ def main():
     u = torch.rand(B, 128)
     fx.update(dict(origin=origin, dir=direction, zc=zc, w=wts, u=u, pts=pts, z=z))
     np.savez_compressed(OUT / "sample_pdf.npz", **{k: v.numpy() for k, v in fx.items()})
+
+    # --- render_with_surface in the atmospheric regime (r03) ---------------------------
+    # sigma in [1e-5, 2e-4] km^-1, 1,024 samples up to 22.7 km (BASELINE configs[2]'s
+    # rays at initialisation): the reference's own function on f64, f32 and f16 tensors,
+    # with dL/d{color, sigma, color_surf} for a loss on color_map alone (the training
+    # loss's path). graphics_utils.py:28 casts z to color.dtype, so the f64 run is the
+    # reference's formula evaluated exactly.
+    g3 = torch.Generator().manual_seed(2026)
+    fx = {}
+    B, N, C = 6, 1024, 4
+    z = (torch.sort(torch.rand(B, N, generator=g3, dtype=torch.float64), dim=1)[0] * 22.7)
+    color = torch.rand(B, N, C, generator=g3, dtype=torch.float64)
+    sigma = torch.exp(torch.empty(B, N, 1, dtype=torch.float64).uniform_(
+        np.log(1e-5), np.log(2e-4), generator=g3))
+    cs = torch.rand(B, C, generator=g3, dtype=torch.float64)
+    gcm = torch.randn(B, C, generator=g3, dtype=torch.float64) * 1e-3
+    fx.update(z=z, color=color, sigma=sigma, cs=cs, gcm=gcm)
+    for tag, dt in [("f64", torch.float64), ("f32", torch.float32), ("f16", torch.float16)]:
+        cc = color.detach().clone().to(dt).requires_grad_(True)
+        ss = sigma.detach().clone().to(dt).requires_grad_(True)
+        css = cs.detach().clone().to(dt).requires_grad_(True)
+        zz = z.float() if dt == torch.float16 else z.to(dt)  # the f16 path gets f32 z
+        zz = zz.detach().clone().requires_grad_(dt != torch.float16)
+        cm, alpha, w, atmo, surf = graphics_utils.render_with_surface(zz, cc, ss, css)
+        cm.backward(gcm.to(dt))
+        fx.update({f"{tag}_cm": cm.detach(), f"{tag}_alpha": alpha.detach(),
+                   f"{tag}_w": w.detach(), f"{tag}_atmo": atmo.detach(),
+                   f"{tag}_surf": surf.detach(), f"{tag}_dcolor": cc.grad,
+                   f"{tag}_dsigma": ss.grad, f"{tag}_dcs": css.grad})
+        if dt != torch.float16:
+            fx[f"{tag}_dz"] = zz.grad
+        if dt == torch.float16:  # the surface product (graphics_utils.py:75) on its own
+            fx["f16_pr"] = (1 - alpha.detach()).prod(dim=1)
+    np.savez_compressed(OUT / "render_atmo.npz",
+                        **{k: v.double().numpy() for k, v in fx.items()})
+
+    # --- the f16 composite and loss the reference's Instant-NGP step runs (r03) ---------
+    # f16 tensors into render_with_surface and mse_plus_hdr etc., gradients through
+    # color_map / the prediction only: the reference's f16 autograd on CPU torch
+    fx = {}
+    for tag, B, N, smax in [("a", 12, 64, 1.0), ("b", 4, 1024, 2e-3)]:
+        z = torch.sort(torch.rand(B, N, generator=g3), dim=1)[0] * 22.7
+        color = torch.rand(B, N, 4, generator=g3).half().requires_grad_(True)
+        sigma = (torch.rand(B, N, 1, generator=g3) * smax).half().requires_grad_(True)
+        cs = torch.rand(B, 4, generator=g3).half().requires_grad_(True)
+        gcm = (torch.randn(B, 4, generator=g3) * 1e-3).half()
+        cm, alpha, w, atmo, surf = graphics_utils.render_with_surface(z, color, sigma, cs)
+        cm.backward(gcm)
+        fx.update({f"{tag}_z": z, f"{tag}_color": color.detach(), f"{tag}_sigma": sigma.detach(),
+                   f"{tag}_cs": cs.detach(), f"{tag}_gcm": gcm, f"{tag}_cm": cm.detach(),
+                   f"{tag}_alpha": alpha.detach(), f"{tag}_w": w.detach(),
+                   f"{tag}_atmo": atmo.detach(), f"{tag}_surf": surf.detach(),
+                   f"{tag}_pr": (1 - alpha.detach()).prod(dim=1),
+                   f"{tag}_dcolor": color.grad, f"{tag}_dsigma": sigma.grad,
+                   f"{tag}_dcs": cs.grad})
+    B = 256
+    pred = (torch.rand(B, generator=g3) * 0.3).half()
+    gt = (torch.rand(B, generator=g3) * 0.3)
+    for mi in (0.37, 61.5):
+        for name in ["dark", "hdr", "l1", "l1_plus_hdr", "mse", "mse_plus_hdr"]:
+            p = pred.clone().requires_grad_(True)
+            val = getattr(losses, f"{name}_loss")(p, gt.half(), mi)
+            val.backward()
+            fx[f"loss_{mi}_{name}_val"], fx[f"loss_{mi}_{name}_grad"] = val.detach(), p.grad
+    fx["loss_pred"], fx["loss_gt"] = pred, gt
+    np.savez_compressed(OUT / "f16_step.npz",
+                        **{k: v.float().numpy() if v.dtype == torch.float16 else v.numpy()
+                           for k, v in fx.items()})
     print("golden vectors written to", OUT)
     for f in sorted(OUT.glob("*.npz")):
         print(f"  {f.name}: {f.stat().st_size / 1024:.1f} KiB")

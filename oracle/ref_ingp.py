@@ -29,10 +29,17 @@ its f16 Instant-NGP path, as opposed to what this build computes:
   f16 tiles (hidden-layer gradients rounded to f16 here), the parameter gradient comes
   back in f16 and is divided by 128, the input gradient likewise;
 * the composite (graphics_utils.py:6-77) runs on those f16 tensors: z is cast to f16
-  km (graphics_utils.py:28), alpha, the cumprod and the sums are f16 torch ops (f32
-  accumulation inside the scan and sums, as torch does on both CPU and GPU);
-* the loss takes the f16 prediction and the target cast to f16 (instant_ngp.py:262);
-  the f16 autograd of the composite and loss rounds every gradient to f16.
+  km (graphics_utils.py:28), alpha, the cumprod and the sums are f16 torch ops, and
+  the f16 autograd of the composite rounds every gradient to f16 -- restated op by op
+  in oracle/ref_f16.py with torch's CUDA accumulation (the reference needs CUDA: f16
+  accumulator in cumprod and in its backward's cumsum, f32 in sum / prod), which
+  differs from torch's CPU f16 kernels (``ref_acc="cpu"`` runs torch's CPU f16 ops
+  instead, for comparison);
+* the loss takes the f16 prediction and the target cast to f16 (instant_ngp.py:262),
+  as f16 ops with their f16 autograd (ref_f16.loss_f16; the Python scalar
+  ``1e-3 * max_i`` added in f32 as torch on CUDA does);
+* a module's parameter gradient is f16(f16(g * 128) / 128): tcnn's f16 gradient at
+  loss scale 128 divided by the loss scale in f16 (``params_grad / loss_scale``).
 Approximations (tcnn absent): the MLP backward's rounding is applied per layer, not per
 16x16 tile; the hash-grid gradient (tcnn: f16 half2 atomics) is summed in f64 and
 rounded once.
@@ -43,7 +50,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import ref_nerf, ref_path, ref_tcnn
+from . import ref_f16, ref_nerf, ref_path, ref_tcnn
 
 MODULES = ("pos_encoder", "pos_mlp", "dir_mlp", "surf_encoder", "surf_mlp")
 
@@ -102,7 +109,7 @@ class _TcnnCall(torch.autograd.Function):
         ins = (x64, p64) if x64.requires_grad else (p64,)
         grads = torch.autograd.grad(y, ins, gs, allow_unused=True)
         gp = grads[-1]
-        gp = torch.zeros_like(p64) if gp is None else gp.half().double() / LOSS_SCALE
+        gp = torch.zeros_like(p64) if gp is None else (gp.half() / LOSS_SCALE).double()
         gx = None
         if x64.requires_grad and grads[0] is not None:
             gx = (grads[0].half().double() / LOSS_SCALE).to(ctx.x_dtype)
@@ -114,7 +121,7 @@ class RefInstantNGP:
 
     def __init__(self, config: dict, state: dict, prep: dict, scale: float, max_i: float,
                  half: bool = False, mlp_half=None, semantics: str = "build",
-                 composite: str = "f32"):
+                 composite: str = "f32", ref_acc: str = "cuda"):
         self.cfg = config
         self.ingp = config["instant_ngp"]
         self.N = int(config["num_samples_per_ray"])
@@ -131,6 +138,9 @@ class RefInstantNGP:
         # "f32": the composite in f32 as the reference evaluates it; "f64": exact, to
         # measure how sensitive a gradient is to the composite's f32 rounding
         self.composite = composite
+        # reference semantics: torch's CUDA ("cuda", ref_f16) or CPU ("cpu", torch ops)
+        # f16 composite / loss kernels
+        self.ref_acc = ref_acc
         self.params = {m: state[m]["params"].detach().cpu().double().clone().requires_grad_(True)
                        for m in MODULES}
         self.pos_grid = _grid_cfg(self.ingp["encoding"], 3)
@@ -239,7 +249,9 @@ class RefInstantNGP:
         color = torch.relu(color.view(B, N, -1))
         color_surf = torch.relu(color_surf)
         sigma = torch.relu(pos_out[:, :1]).view(B, N, 1)
-        cm, alpha, weights, atmo, surf = ref_path.render_with_surface(
+        render = (ref_path.render_with_surface if self.ref_acc == "cpu" else
+                  lambda *a: ref_f16.render_with_surface(*a, acc=self.ref_acc))
+        cm, alpha, weights, atmo, surf = render(
             z * (self.scale / 1000), color, sigma, color_surf)  # f16 (z cast inside)
         return {"color_map_fine": cm, "color_map_atmo": atmo, "color_map_surf": surf,
                 "weights_fine": weights, "z_vals_fine": z, "color_fine": color[:, :-1],
@@ -250,6 +262,8 @@ class RefInstantNGP:
         (the target cast to the prediction's dtype, :262)."""
         pred = torch.take_along_dim(res["color_map_fine"], b["irgb_idx"][:, None], 1)[:, 0]
         gt = b["rad"].to(pred.dtype) if pred.dtype == torch.float16 else b["rad"].double()
+        if self.semantics == "reference" and self.ref_acc != "cpu":
+            return ref_f16.LossF16.apply(pred, gt, self.max_i, name, self.ref_acc)
         return ref_path.LOSSES[name](pred, gt, self.max_i)
 
     def optimizer(self, opt_cfg: dict) -> torch.optim.Optimizer:

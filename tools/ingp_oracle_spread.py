@@ -1,0 +1,77 @@
+"""Spread of the reference-semantics Instant-NGP oracle under one f16 rounding (CPU only).
+
+Trains oracle/ref_ingp.RefInstantNGP(semantics="reference") exactly as
+tests/test_ingp_oracle_gpu.py::test_psnr_vs_reference_semantics does (8-view 16x16 scene,
+batch 256, 64 samples per ray, AdamW of configs/instant_ngp.json, same batches and draws),
+once unperturbed and once per perturbation k (tests/ingp_psnr.OracleRunner):
+``--perturb grad``: at the first step the f16 loss gradient reaching ray k's rendered
+colour is moved by one f16 ulp -- one rounding of the reference's f16 backward done the
+other way; ``--perturb dirs``: every ray direction moved by one f32 ulp (seed k) -- the
+size of the host-vs-device libm differences of scene construction. Prints the PSNR at
+0/8/16/32/64 iterations for every run (JSON with --out).
+
+    python tools/ingp_oracle_spread.py [--runs 3] [--out profiles/r03_ingp_oracle_spread.json]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "atmospheric-neural-rendering_amd")]
+
+import torch  # noqa: E402
+
+from oracle import ref_ingp  # noqa: E402
+from tests import ingp_psnr  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--runs", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=64)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--semantics", default="reference")
+    ap.add_argument("--ref-acc", default="cuda", help="cuda | cpu (oracle/ref_ingp.py)")
+    ap.add_argument("--perturb", default="grad", help="grad: one f16 ulp of one ray's "
+                    "loss gradient at step 0; dirs: every ray direction by one f32 ulp")
+    a = ap.parse_args()
+    torch.set_num_threads(a.threads)
+    import __graft_entry__ as ge
+    from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
+    from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
+
+    scene = SyntheticHARP2Dataset(n_views=8, img_size=16, device=torch.device("cpu"), seed=0)
+    cfg = ge._ingp_config(64)
+    p = InstantNGPPipeline(cfg, scene, dtype=torch.float16, fused=True, seed=5)
+    state = p.state_dict()
+    pp = scene.get_point_preprocessor("horizontal")
+    opt = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
+    runners = {}
+    for run in range(-1, a.runs):
+        o = ref_ingp.RefInstantNGP(cfg, state, ref_ingp.prep_kwargs(pp), p.scale, scene.max_i,
+                                   half=True, semantics=a.semantics, ref_acc=a.ref_acc)
+        if run < 0:
+            runners["unperturbed"] = ingp_psnr.OracleRunner(o, opt)
+        elif a.perturb == "grad":
+            runners[f"perturb_ray{run}"] = ingp_psnr.OracleRunner(o, opt, perturb_ray=run)
+        else:
+            runners[f"perturb_dirs{run}"] = ingp_psnr.OracleRunner(o, opt, perturb_dirs=run)
+    t0 = time.time()
+    cps = tuple(c for c in ingp_psnr.CHECKPOINTS if c <= a.iters)
+    res = ingp_psnr.train_side_by_side(runners, scene, 64, checkpoints=cps)
+    for name, out in res.items():
+        print(name, [round(r["psnr"], 4) for r in out], flush=True)
+    print(f"{time.time() - t0:.0f}s")
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

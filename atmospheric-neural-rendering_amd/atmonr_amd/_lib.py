@@ -471,6 +471,10 @@ def compute_copy(param: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     writes it in the same pass as the parameter update and marks it current.
     """
     if param.dtype == dtype:
+        if getattr(param, "_anr_master_stale", False):
+            raise ANRError("f32 compute from a parameter whose f32 master is stale "
+                           "(ShardedAdam gather='f16' keeps only the f16 copies current: "
+                           "use gather='f32' for f32 modules, or consolidate())")
         return param.detach()
     sh = getattr(param, "_anr_shadow", None)
     if sh is None or sh.dtype != dtype or sh.device != param.device or sh.shape != param.shape:
@@ -481,6 +485,18 @@ def compute_copy(param: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
         sh.copy_(param.detach())
         param._anr_shadow_ver = param._version
     return sh
+
+
+def pack_source(param: torch.Tensor, mma_dtype: int) -> torch.Tensor:
+    """The f32 values the fused field packs its MFMA weight fragments from: the f32 master,
+    or -- when a ShardedAdam with gather='f16' left this rank's master slice stale -- the
+    current f16 compute copy (identical after the pack's f16 rounding)."""
+    if getattr(param, "_anr_master_stale", False):
+        if mma_dtype != F16:
+            raise ANRError("bf16 field weights need current f32 masters "
+                           "(ShardedAdam gather='f32', or consolidate())")
+        return compute_copy(param, torch.float16).float()
+    return param.detach().float()
 
 
 def hashgrid_desc(n_dims: int, n_levels: int, n_features: int, base_resolution: int,

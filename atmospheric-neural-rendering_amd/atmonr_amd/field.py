@@ -83,7 +83,7 @@ class IngpFieldFn(torch.autograd.Function):
             pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
             packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc),
                                  device=dev, dtype=torch.float16)  # 16-bit carrier
-            m_pos, m_dir = p_pos.detach().float(), p_dir.detach().float()  # f32 masters
+            m_pos, m_dir = _lib.pack_source(p_pos, mma), _lib.pack_source(p_dir, mma)
             call("anr_ingp_field_pack", pdesc, ddesc, mma, ptr(m_pos), ptr(m_dir), ptr(packed),
                  s, tag="field_pack")
             nb = pipe.dir_mlp.n_output_dims
@@ -195,6 +195,8 @@ class IngpFieldFn(torch.autograd.Function):
                      ptr(d_color), d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos),
                      ptr(g_dir), ptr(ws), ws_bytes, s, tag="field_bwd")
         _done(direct_p, p_pos, direct_d, p_dir)  # MLP grads final: their all-reduce may start
+        if getattr(pipe, "_keep_d_enc", False):  # diagnostics (tools/ref16_field_diag.py)
+            pipe._last_d_enc = d_enc
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
         _done(direct_h, p_hash)
@@ -214,7 +216,8 @@ def field_fused(pipe) -> bool:
               and pipe.dir_mlp.dtype == pipe.pos_mlp.dtype
               and (pipe.pos_mlp.dtype == torch.float16
                    or pipe.pos_encoder.dtype == torch.float16)
-              and getattr(pipe, "allow_field_fusion", True))
+              and getattr(pipe, "allow_field_fusion", True)
+              and getattr(pipe, "fused", True))  # fused=False: the unfused parity path
         if ok:
             ok = bool(_lib.load().anr_ingp_field_supported(ctypes.byref(pipe.pos_mlp.desc),
                                                            ctypes.byref(pipe.dir_mlp.desc)))
@@ -246,8 +249,8 @@ def field_density(pipe, pts: torch.Tensor) -> torch.Tensor:
     pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
     packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc), device=dev,
                          dtype=torch.float16)
-    call("anr_ingp_field_pack", pdesc, ddesc, mma, ptr(pos_mod.params.detach().float()),
-         ptr(pipe.dir_mlp.params.detach().float()), ptr(packed), s, tag="field_pack")
+    call("anr_ingp_field_pack", pdesc, ddesc, mma, ptr(_lib.pack_source(pos_mod.params, mma)),
+         ptr(_lib.pack_source(pipe.dir_mlp.params, mma)), ptr(packed), s, tag="field_pack")
     dirs = torch.full((1, 3), 0.5, device=dev)  # one "ray" for all points: colour unused
     color = torch.empty(P, pipe.dir_mlp.n_output_dims, device=dev, dtype=torch.float32)
     call("anr_ingp_field_fwd", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc.stride(0),

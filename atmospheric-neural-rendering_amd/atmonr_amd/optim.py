@@ -36,11 +36,12 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        batches: dict = {}  # device -> [anr_adam_tensor]
+        # (device, beta1, beta2, eps) -> [anr_adam_tensor]: groups with their own betas /
+        # eps get their own launch, as torch.optim.Adam(W) steps each group with its own
+        batches: dict = {}
         for group in self.param_groups:
             b1, b2 = group["betas"]
-            if (b1, b2, group["eps"]) != self._shared(group):
-                raise _lib.ANRError("FusedAdam: betas / eps must be equal across param groups")
+            key_hp = (float(b1), float(b2), float(group["eps"]))
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -67,31 +68,22 @@ class FusedAdam(torch.optim.Optimizer):
                                     ptr(st["exp_avg_sq"]), ptr(sh), p.numel(),
                                     float(group["lr"]), float(group["weight_decay"]),
                                     int(st["step"].item()))
-                batches.setdefault(p.device, []).append(t)
+                batches.setdefault((p.device,) + key_hp, []).append(t)
                 if sh is not None:
                     p._anr_shadow_ver = p._version
-        b1, b2 = self.defaults["betas"]
-        eps = self.defaults["eps"]
-        if self.param_groups:
-            b1, b2 = self.param_groups[0]["betas"]
-            eps = self.param_groups[0]["eps"]
-        for dev, ts in batches.items():
+        for (dev, b1, b2, eps), ts in batches.items():
             if self.multi_tensor:
                 arr = (_lib.AdamTensor * len(ts))(*ts)
-                call("anr_adam_step_multi", ctypes.addressof(arr), len(ts), float(b1), float(b2),
-                     float(eps), int(self.decoupled), int(self.zero_grad_in_step),
-                     _lib.stream(dev))
+                call("anr_adam_step_multi", ctypes.addressof(arr), len(ts), b1, b2, eps,
+                     int(self.decoupled), int(self.zero_grad_in_step), _lib.stream(dev))
             else:
                 for t in ts:
                     call("anr_adam_step", t.params, t.grad, t.exp_avg, t.exp_avg_sq,
-                         t.params_f16, t.n, t.lr, float(b1), float(b2), float(eps),
-                         t.weight_decay, int(self.decoupled), t.step,
-                         int(self.zero_grad_in_step), _lib.stream(dev))
+                         t.params_f16, t.n, t.lr, b1, b2, eps, t.weight_decay,
+                         int(self.decoupled), t.step, int(self.zero_grad_in_step),
+                         _lib.stream(dev))
         if self.zero_grad_in_step:
             for b in self.zeroed_buckets:
                 b.mark_zero()
         return loss
 
-    def _shared(self, group):
-        g0 = self.param_groups[0]
-        return (g0["betas"][0], g0["betas"][1], g0["eps"])

@@ -31,9 +31,13 @@ import torch.distributed as dist
 
 
 class FlatGradBucket:
-    def __init__(self, params: Iterable[torch.nn.Parameter], device=None):
+    def __init__(self, params: Iterable[torch.nn.Parameter], device=None, pad_to: int = 1):
+        """``pad_to``: round the buffer up to a multiple (ShardedAdam's rank count; the
+        tail past the last parameter stays zero)."""
         self.params = [p for p in params if p.requires_grad]
         n = sum(p.numel() for p in self.params)
+        self.n_params = n
+        n = -(-n // pad_to) * pad_to
         dev = device if device is not None else self.params[0].device
         self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
         self._known_zero = True
@@ -168,3 +172,160 @@ class FlatGradBucket:
     @property
     def numel(self) -> int:
         return self.flat.numel()
+
+
+class ShardSegment:
+    """The part of one parameter inside this rank's shard: views into the flat buffers
+    (``param``, ``grad``, ``exp_avg``, ``exp_avg_sq``, ``shadow`` f16 or None) and its
+    group's ``lr`` / ``weight_decay``."""
+
+    __slots__ = ("param", "grad", "exp_avg", "exp_avg_sq", "shadow", "lr", "weight_decay")
+
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+def hip_adam_update(segments, step: int, betas, eps: float, decoupled: bool) -> None:
+    """Adam(W) over the shard's segments in one anr_adam_step_multi launch (the K10
+    kernel FusedAdam uses)."""
+    import ctypes
+
+    from . import _lib
+
+    if not segments:
+        return
+    ts = [_lib.AdamTensor(_lib.ptr(s.param), _lib.ptr(s.grad), _lib.ptr(s.exp_avg),
+                          _lib.ptr(s.exp_avg_sq), _lib.ptr(s.shadow), s.param.numel(),
+                          float(s.lr), float(s.weight_decay), int(step)) for s in segments]
+    arr = (_lib.AdamTensor * len(ts))(*ts)
+    dev = segments[0].param.device
+    _lib.call("anr_adam_step_multi", ctypes.addressof(arr), len(ts), float(betas[0]),
+              float(betas[1]), float(eps), int(decoupled), 0, _lib.stream(dev), tag="adam")
+
+
+class ShardedAdam:
+    """Optimizer sharded over the data-parallel ranks (ZeRO stage 1), the alternative to
+    FlatGradBucket.all_reduce + a replicated FusedAdam:
+
+    1. ``reduce_scatter(AVG)`` of the flat gradient bucket: rank r receives the averaged
+       gradient of its slice [r*S, (r+1)*S) of the flat parameter vector;
+    2. Adam(W) on that slice only (state for 1/W of the parameters; per-parameter lr and
+       weight decay of its param group, as the replicated optimizer);
+    3. ``all_gather`` of the updated slice: ``gather="f16"`` gathers the f16 compute copy
+       the forward kernels read (half the bytes of f32; the f32 masters outside the slice
+       are then stale until :meth:`consolidate`, which checkpoints call), ``gather="f32"``
+       gathers the f32 parameters (every replica stays complete; the f16 copies refresh
+       from them on the next forward).
+
+    Bytes per step: reduce-scatter 4n + all-gather 2n (f16) against the all-reduce's 8n
+    (a ring all-reduce is a reduce-scatter plus an all-gather of f32), and the AdamW pass
+    over n / W elements. Parameters become views into one flat f32 buffer (padded to a
+    multiple of W). ``update(segments, step, betas, eps, decoupled)`` applies the update
+    (default: the HIP multi-tensor kernel; tests inject a reference)."""
+
+    def __init__(self, bucket: FlatGradBucket, param_groups: list, betas=(0.9, 0.999),
+                 eps: float = 1e-8, decoupled: bool = True, gather: str = "f16", group=None,
+                 update=hip_adam_update):
+        if gather not in ("f16", "f32"):
+            raise ValueError("gather: 'f16' or 'f32'")
+        self.bucket, self.group, self.gather = bucket, group, gather
+        self.betas, self.eps, self.decoupled = tuple(betas), float(eps), decoupled
+        self.update = update
+        self.world = dist.get_world_size(group) if bucket._distributed(group) else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        n_pad = bucket.flat.numel()
+        if n_pad % self.world:
+            raise ValueError("FlatGradBucket must be padded to a multiple of the rank count "
+                             "(FlatGradBucket(..., pad_to=world_size))")
+        self.S = n_pad // self.world
+        dev = bucket.flat.device
+        hp = {}
+        for g in param_groups:
+            for p in g["params"]:
+                hp[id(p)] = (float(g.get("lr", 1e-3)), float(g.get("weight_decay", 0.0)))
+        # flat f32 parameters: every parameter becomes a view into it
+        self.flat_param = torch.zeros(n_pad, device=dev, dtype=torch.float32)
+        off = 0
+        self._spans = []  # (param, offset)
+        with torch.no_grad():
+            for p in bucket.params:
+                if id(p) not in hp:
+                    raise ValueError("every bucketed parameter must be in a param group")
+                n = p.numel()
+                self.flat_param[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat_param[off:off + n].view_as(p)
+                self._spans.append((p, off))
+                off += n
+        lo, hi = self.rank * self.S, (self.rank + 1) * self.S
+        self.grad_shard = torch.zeros(self.S, device=dev, dtype=torch.float32)
+        self.exp_avg = torch.zeros(self.S, device=dev, dtype=torch.float32)
+        self.exp_avg_sq = torch.zeros(self.S, device=dev, dtype=torch.float32)
+        self.flat_shadow = self.shadow_shard = None
+        if gather == "f16":
+            self.flat_shadow = self.flat_param.to(torch.float16)
+            self.shadow_shard = torch.zeros(self.S, device=dev, dtype=torch.float16)
+            for p, o in self._spans:
+                p._anr_shadow = self.flat_shadow[o:o + p.numel()].view_as(p)
+                p._anr_shadow_ver = p._version
+        self.segments = []
+        for p, o in self._spans:
+            a, b = max(o, lo), min(o + p.numel(), hi)
+            if a >= b:
+                continue
+            lr, wd = hp[id(p)]
+            self.segments.append(ShardSegment(
+                param=self.flat_param[a:b], grad=self.grad_shard[a - lo:b - lo],
+                exp_avg=self.exp_avg[a - lo:b - lo], exp_avg_sq=self.exp_avg_sq[a - lo:b - lo],
+                shadow=None if self.shadow_shard is None else self.shadow_shard[a - lo:b - lo],
+                lr=lr, weight_decay=wd))
+        self.steps = 0
+        self.masters_current = True
+
+    @torch.no_grad()
+    def step(self) -> None:
+        """Reduce-scatter, update this rank's slice, all-gather (call after backward, in
+        place of bucket.all_reduce() + optimizer.step())."""
+        lo = self.rank * self.S
+        if self.world > 1:
+            dist.reduce_scatter_tensor(self.grad_shard, self.bucket.flat, op=dist.ReduceOp.AVG,
+                                       group=self.group)
+        else:
+            self.grad_shard.copy_(self.bucket.flat[lo:lo + self.S])
+        self.steps += 1
+        self.update(self.segments, self.steps, self.betas, self.eps, self.decoupled)
+        mine = self.flat_param[lo:lo + self.S]
+        if self.gather == "f16":
+            if self.world > 1:
+                dist.all_gather_into_tensor(self.flat_shadow, self.shadow_shard, group=self.group)
+            else:
+                self.flat_shadow.copy_(self.shadow_shard)
+            self.masters_current = self.world == 1
+            for p, _ in self._spans:
+                p._anr_shadow_ver = p._version  # the gathered f16 copy is current
+                p._anr_master_stale = not self.masters_current
+        else:
+            if self.world > 1:
+                dist.all_gather_into_tensor(self.flat_param, mine.clone(), group=self.group)
+            for p, _ in self._spans:
+                if hasattr(p, "_anr_shadow_ver"):
+                    p._anr_shadow_ver = None  # refresh the f16 copy from the gathered f32
+        self.bucket._known_zero = False
+
+    @torch.no_grad()
+    def consolidate(self) -> None:
+        """All-gather the f32 master slices so every replica holds every parameter (before
+        a checkpoint or an evaluation on the f32 weights; f16 gather only)."""
+        if self.masters_current:
+            return
+        lo = self.rank * self.S
+        dist.all_gather_into_tensor(self.flat_param, self.flat_param[lo:lo + self.S].clone(),
+                                    group=self.group)
+        self.masters_current = True
+        for p, _ in self._spans:
+            p._anr_master_stale = False
+            if hasattr(p, "_anr_shadow_ver"):
+                p._anr_shadow_ver = p._version
+
+    def state_numel(self) -> int:
+        return 2 * self.S

@@ -276,8 +276,9 @@ class InstantNGPPipeline(Pipeline):
             pts[..., 2] = pts[..., 2] / self.alt_compress
         if self.num_density_outputs == 1 and field_fused(self) and \
                 self.pos_encoder.dtype == torch.float16:
-            # the fused field's sigma output IS relu(pos_out[:, 0])
-            return field_density(self, pts).view(pts.shape[0], 1)
+            # the fused field's sigma output IS relu(pos_out[:, 0]) (f32 accumulator);
+            # returned in tcnn's output precision, as the reference's clip of pos_out
+            return field_density(self, pts).view(pts.shape[0], 1).to(self.pos_mlp.output_dtype)
         with torch.no_grad():
             pos_out = self.pos_mlp(self.pos_encoder(pts))
         return torch.clip(pos_out[..., : self.num_density_outputs].view(

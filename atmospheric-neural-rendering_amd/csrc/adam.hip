@@ -126,6 +126,14 @@ extern "C" int anr_adam_step_multi(const anr_adam_tensor* tensors, int32_t n_ten
                                    int32_t zero_grad, anr_stream_t stream) {
   using namespace anr;
   ANR_CHECK_ARG(n_tensors >= 0 && (n_tensors == 0 || tensors), "anr_adam_step_multi: bad tensors");
+  // every descriptor is checked before the first launch: a bad tensor after the first
+  // ANR_ADAM_MAX_TENSORS must not leave the earlier ones updated (a partial step)
+  for (int32_t i = 0; i < n_tensors; ++i) {
+    const anr_adam_tensor& d = tensors[i];
+    ANR_CHECK_ARG(d.n >= 0 && d.step >= 1, "anr_adam_step_multi: tensor %d: bad size/step", i);
+    ANR_CHECK_ARG(d.n == 0 || (d.params && d.grad && d.exp_avg && d.exp_avg_sq),
+                  "anr_adam_step_multi: tensor %d: null pointer", i);
+  }
   int32_t t = 0;  // next tensor to place (empty tensors take no slot)
   while (t < n_tensors) {
     AdamTensors a;

@@ -50,6 +50,20 @@ def measured_peaks(dev, spec: bool) -> dict:
     return p
 
 
+def pmc_entry(pmc: dict, tag: str, key_sfx: str):
+    """(entry, stale) of profiles/pmc_traffic.json for a kernel tag: an entry measured on a
+    different version of the kernel's source (sha1 stamped by tools/prof_summary.py) is
+    stale and must not price this build's kernel."""
+    ent = (pmc or {}).get(f"{tag}:{key_sfx}")
+    if not ent:
+        return None, False
+    from tools.prof_summary import source_sha1
+
+    if ent.get("kernel_source_sha1") != source_sha1(tag):
+        return ent, True
+    return ent, False
+
+
 def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "") -> dict:
     """Algorithmic work per launch of each hot kernel.
 
@@ -83,9 +97,14 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "") -> d
         # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; forward recompute + dX + dW
         "field_bwd": {"bytes": M * (enc_b + 4 * nb + 4 + 4 * grid.n_out), "flops": 3 * M * f_fwd},
     }
-    ent = (pmc or {}).get(f"hash_bwd:{key_sfx}")
-    if ent and ent.get("atomic_requests"):
+    ent, stale = pmc_entry(pmc, "hash_bwd", key_sfx)
+    if ent and ent.get("atomic_requests") and not stale:
         out["hash_bwd"]["atomic_requests"] = float(ent["atomic_requests"])
+        out["hash_bwd"]["atomic_requests_source"] = (
+            f"profiles/pmc_traffic.json [{ent.get('source')}], rocprofv3 --pmc "
+            "TCC_EA0_ATOMIC_sum of this kernel source (sha1 match)")
+    elif ent and ent.get("atomic_requests"):
+        out["hash_bwd"]["atomic_requests_stale"] = ent.get("source")
     return out
 
 
@@ -291,6 +310,11 @@ def main():
                     help="zero the gradient bucket with a fill instead of in the AdamW pass")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one all-reduce of the whole gradient bucket after backward")
+    ap.add_argument("--shard-optimizer", choices=["off", "f16", "f32"], default="off",
+                    help="ZeRO-1 (atmonr_amd.parallel.ShardedAdam): reduce-scatter of the "
+                         "gradient, AdamW on 1/N of the parameters, all-gather of the f16 "
+                         "compute copy (f16) or of the f32 parameters (f32), instead of "
+                         "all-reduce + replicated AdamW")
     ap.add_argument("--field-bwd", choices=["rt", "lds"], default="rt",
                     help="fused field backward generation (anr_ingp_field_force_bwd): "
                          "register-transposed (default) or LDS-staged tiles")
@@ -357,14 +381,19 @@ def main():
 
     # one flat f32 gradient bucket; every param's .grad is a view into it, so backward
     # accumulates in place and DP needs exactly one all-reduce per step
-    from atmonr_amd.parallel import FlatGradBucket
+    from atmonr_amd.parallel import FlatGradBucket, ShardedAdam
 
-    bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev)
+    sharded = args.shard_optimizer != "off"
+    bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev,
+                            pad_to=world)
     if world > 1:
         bucket.broadcast_params(0)  # replicas start from rank 0's weights
-    if not args.no_fused_zero:
+    if sharded:
+        opt = ShardedAdam(bucket, opt.param_groups, betas=opt_cfg["betas"], eps=opt_cfg["eps"],
+                          gather=args.shard_optimizer)
+    elif not args.no_fused_zero:
         bucket.fuse_zero_into(opt)  # the AdamW pass zeroes the bucket (no per-step fill)
-    if not args.no_overlap:
+    if not args.no_overlap and not sharded:
         # each chunk's all-reduce starts once its gradients are final: the surface and MLP
         # gradients reduce while the hash-grid backward runs
         bucket.enable_overlap()
@@ -386,8 +415,9 @@ def main():
         loss = pipe.compute_loss(batch, res)
         bucket.zero()
         loss.backward()
-        bucket.all_reduce()
-        opt.step()
+        if not sharded:
+            bucket.all_reduce()
+        opt.step()  # ShardedAdam: reduce-scatter, sharded AdamW, all-gather
         return loss
 
     for _ in range(args.warmup):
@@ -410,7 +440,8 @@ def main():
             pmc = json.load(open(pmc_path))
         except (OSError, ValueError):
             pmc = {}
-    pmc_sfx = f"{args.variant}:{rank_batch}x{args.samples}"
+    pmc_sfx = (f"{args.variant}{'' if args.dtype == 'f16' else '-' + args.dtype}:"
+               f"{rank_batch}x{args.samples}")
     models = kernel_models(pipe, M, pmc, pmc_sfx)
     kernels, dominant = {}, None
     if not args.no_kernel_timer:
@@ -500,7 +531,7 @@ def main():
                 ach, peak, frac, unit = k["hbm_gbs"], peaks["hbm_copy_gbs"], k["hbm_frac"], "GB/s"
             else:
                 ach, peak, frac, unit = k["mfma_tfs"], peaks[mfma_key], k["mfma_frac"], "TFLOP/s"
-            roofline = {"kernel": dominant, "bound": "hbm" if bound == "atomic" else bound,
+            roofline = {"kernel": dominant, "bound": bound,
                         "ceiling": ("memory-side f32 atomic requests (MI355X_MICROARCH.md "
                                     "'Global float atomics'), measured at 16-B segments"
                                     if bound == "atomic" else
@@ -515,14 +546,22 @@ def main():
                                                         "survey_model_frac") if x in k}}
             if "atomic_requests" in mdl:
                 roofline["atomic_requests_per_launch"] = mdl["atomic_requests"]
+                roofline["atomic_requests_source"] = mdl["atomic_requests_source"]
+            if "atomic_requests_stale" in mdl:
+                roofline["atomic_requests_stale"] = (
+                    f"PMC entry {mdl['atomic_requests_stale']} measured on another version of "
+                    "the kernel source: not used (bound priced on bytes)")
             if "survey_bytes" in mdl:
                 # SURVEY §8(d)'s per-sample model (every corner access as HBM bytes)
                 roofline["survey_model"] = {
                     "bytes_per_unit": mdl["survey_bytes"] / M,
                     "achieved": k["survey_model_gbs"], "frac": k["survey_model_frac"]}
-            ent = pmc.get(f"{dominant}:{pmc_sfx}")
-            if ent:  # HBM bytes per launch from rocprofv3 PMC (tools/prof.sh)
+            ent, stale = pmc_entry(pmc, dominant, pmc_sfx)
+            if ent and stale:
+                roofline["traffic_stale"] = ent.get("source")
+            elif ent:  # HBM bytes per launch from rocprofv3 PMC (tools/prof.sh)
                 roofline["traffic"] = ent["bytes"]
+                roofline["traffic_source"] = f"profiles/pmc_traffic.json [{ent.get('source')}]"
                 roofline["traffic_frac_of_measured_hbm"] = round(
                     ent["bytes"] / (st["avg_ms"] * 1e-3) / 1e9 / peaks["hbm_copy_gbs"], 4)
 
@@ -571,10 +610,15 @@ def main():
             "peaks": peaks,
             "kernels": kernels,
             "kernels_source": f"untimed profiling pass of {args.profile_steps} steps",
-            "grad_all_reduce": {
+            "grad_all_reduce": None if sharded else {
                 "bytes": 4 * bucket.numel, "overlap": bucket.overlap,
                 "chunks": len(bucket._chunks) if bucket.overlap else 1,
                 "issued_during_backward": bucket.early_issued if bucket.overlap else 0,
+                "backend": dist.get_backend() if world > 1 else None},
+            "sharded_optimizer": None if not sharded else {
+                "reduce_scatter_bytes": 4 * bucket.numel,
+                "all_gather_bytes": (2 if args.shard_optimizer == "f16" else 4) * bucket.numel,
+                "state_floats_per_rank": opt.state_numel(), "gather": args.shard_optimizer,
                 "backend": dist.get_backend() if world > 1 else None},
             "occupancy": None if occ is None else {
                 "grid": list(occ.res), "threshold": occ.threshold, "warmup": occ.warmup,

@@ -144,9 +144,12 @@ int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x, int64_t x_strid
                      int64_t M, const void* table, int32_t table_dtype, void* out,
                      int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
 
-/* Kernel generation: 0 = default (forward v1 one-lane-per-level, backward v2
- * four-lanes-per-level), 1 = v1 both, 2 = v2 both, 3 = forward v3 (batched gathers, F = 2)
- * + backward v2. Test hook; process-wide. Returns the previous mode. */
+/* Kernel generation (test / A-B hook; process-wide; returns the previous mode; also
+ * ANR_HASHGRID_MODE): 0 = default (forward v6 branch-free walker -- v1 above 16 levels or
+ * past 32-bit buffer offsets -- backward v2 four-lanes-per-level), 1 = v1 both,
+ * 2 = v2 both, 3 = forward v3 (batched gathers, F = 2) + backward v2, 4 / 5 = forward v4
+ * (per sample) / v5 (LDS-compacted gathers) + backward v2, 6 = forward v1 + backward v2
+ * (the r01 default), 7 = mode 0 with the backward's run-time-stride instantiation. */
 int anr_hashgrid_force_v1(int32_t mode);
 
 /* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)

@@ -1,8 +1,10 @@
 """ORACLE (test infrastructure only): time the configs/nerf.json CPU train step.
 
 bench.py's ``cpu_baseline`` leg: the reference's own CPU-runnable configuration
-(BASELINE.json configs[0]: nerf.json on an 8-view 64x64 synthetic scene, batch 4096),
-run with oracle/ref_nerf.py on the host cores. Returns rays/s over a bounded sample.
+(BASELINE.json configs[0]: nerf.json's pipeline on an 8-view 64x64 synthetic scene), run
+with oracle/ref_nerf.py on the host cores at batch 1,024 (nerf.json trains at 4,096;
+rays/s of the NeRF step is flat in the batch on the CPU, SURVEY §6: 280-360 at 256 and
+~350 at 4,096) so the bounded sample fits bench.py's time budget. Returns rays/s.
 """
 
 from __future__ import annotations

@@ -17,8 +17,11 @@ Restates src/atmonr/pipelines/instant_ngp.py:137-206 (forward) and :249-263
 
 ``half=True`` rounds what the f16 GPU path rounds (hash table, encodings, MLP weights
 and hidden activations, the f16 MLP outputs) so the oracle tracks the bench
-configuration; gradients pass through the roundings unchanged (casts are identity in
-autograd). tcnn semantics are unpinned against real tinycudann (see ref_tcnn).
+configuration; the roundings act on values only, gradients pass through them in f64
+(ref_tcnn.rounder; r02's plain ``.half().double()`` casts quantised the UNSCALED
+gradients to f16 in autograd, so that oracle's "exact" f16-forward gradients carried
+f16 underflow of their own). tcnn semantics are unpinned against real tinycudann (see
+ref_tcnn).
 
 ``semantics="reference"`` (with ``half=True``) restates what the REFERENCE computes in
 its f16 Instant-NGP path, as opposed to what this build computes:
@@ -147,7 +150,7 @@ class RefInstantNGP:
         self.surf_grid = _grid_cfg(self.ingp["surface_encoding"]["nested"][0], 2)
 
     def _rnd(self, t):
-        return t.half().double() if self.half else t
+        return ref_tcnn.rounder(self.half)(t)
 
     def _mlp(self, x, p, n_in, n_out, net_cfg, half=None):
         half = self.half if half is None else half

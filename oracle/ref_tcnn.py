@@ -153,12 +153,28 @@ def mlp_layer_shapes(n_in, n_out, width, n_hidden):
     return shapes, nip, nop
 
 
+class _RoundValue(torch.autograd.Function):
+    """x -> float64(dtype(x)) forward; the gradient passes through UNCHANGED. (A plain
+    ``t.half().double()`` is not that: autograd casts the incoming gradient back through
+    f16, quantising small unscaled gradients -- the r02 oracle's f16 "exact" gradients
+    were rounded that way.)"""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        return x.to(dtype).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
 def rounder(half):
-    """float64 -> the kernel's 16-bit operand type -> float64 (identity for half=False)."""
+    """float64 -> the kernel's 16-bit operand type -> float64 on the VALUES (identity for
+    half=False); gradients flow through in full precision."""
     if half == "bf16":
-        return lambda t: t.to(torch.bfloat16).double()
+        return lambda t: _RoundValue.apply(t, torch.bfloat16)
     if half:
-        return lambda t: t.half().double()
+        return lambda t: _RoundValue.apply(t, torch.float16)
     return lambda t: t
 
 

@@ -220,3 +220,114 @@ def test_loader_iterates_tail_shares():
     assert {g[1].numel() for g in got} == {25}
     allidx = torch.cat([t for g in got for t in g])
     assert allidx.unique().numel() == 1000
+
+
+def _reference_adamw(segments, step, betas, eps, decoupled):
+    """The K10 kernel's arithmetic (adam.hip) in torch, for the CPU tests of ShardedAdam."""
+    import math
+
+    b1, b2 = betas
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    for s in segments:
+        p, g = s.param, s.grad
+        if s.weight_decay:
+            p.mul_(1 - s.lr * s.weight_decay)
+        s.exp_avg.lerp_(g, 1 - b1)
+        s.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (s.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(s.exp_avg, denom, value=-s.lr / bc1)
+        if s.shadow is not None:
+            s.shadow.copy_(p)
+
+
+def _sharded_worker(rank, world, port, gather, out):
+    import sys
+
+    from tests.conftest import PKG
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from atmonr_amd.parallel import FlatGradBucket, ShardSegment, ShardedAdam
+
+    sizes = [37, 5, 1000, 3, 129]  # shards straddle parameter boundaries
+
+    def make():
+        g = torch.Generator().manual_seed(1)
+        return [torch.nn.Parameter(torch.randn(n, generator=g) * 0.1) for n in sizes]
+
+    def groups(ps):  # as InstantNGPPipeline.get_optimizer: two groups, wd on the second
+        return [{"params": ps[:2], "weight_decay": 0.0, "lr": 1e-2},
+                {"params": ps[2:], "weight_decay": 1e-2, "lr": 3e-3}]
+
+    def loss_of(ws, step):
+        x = torch.randn(16, sum(sizes), generator=torch.Generator().manual_seed(100 * step + rank))
+        w = torch.cat([t.reshape(-1) for t in ws])
+        return ((x * w).sum(1) ** 2).mean() + (w ** 3).sum()
+
+    betas, eps = (0.9, 0.99), 1e-15
+    # (a) all-reduce of the flat bucket + the replicated update over whole parameters
+    pa = make()
+    ba = FlatGradBucket(pa, device=torch.device("cpu"))
+    hp = {id(p): (g["lr"], g["weight_decay"]) for g in groups(pa) for p in g["params"]}
+    st = {id(p): (torch.zeros_like(p), torch.zeros_like(p)) for p in pa}
+    # (b) ShardedAdam
+    pb = make()
+    bb = FlatGradBucket(pb, device=torch.device("cpu"), pad_to=world)
+    opt = ShardedAdam(bb, groups(pb), betas=betas, eps=eps, gather=gather,
+                      update=_reference_adamw)
+    for step in range(1, 5):
+        # forward on what the kernels would read: the f16 copy in gather="f16" mode
+        fa = [p.detach().half().float().requires_grad_(False) if gather == "f16" else p
+              for p in pa]
+        if gather == "f16":
+            for p, f in zip(pa, fa):
+                f.requires_grad_(True)
+        ba.zero()
+        la = loss_of(fa, step)
+        la.backward()
+        if gather == "f16":
+            for p, f in zip(pa, fa):
+                p.grad.copy_(f.grad)
+        ba.all_reduce()
+        with torch.no_grad():
+            segs = [ShardSegment(param=p.data.view(-1), grad=p.grad.view(-1),
+                                 exp_avg=st[id(p)][0].view(-1), exp_avg_sq=st[id(p)][1].view(-1),
+                                 shadow=None, lr=hp[id(p)][0], weight_decay=hp[id(p)][1])
+                    for p in pa]
+            _reference_adamw(segs, step, betas, eps, True)
+        fb = [p._anr_shadow.float().requires_grad_(True) if gather == "f16" else p for p in pb]
+        bb.zero()
+        lb = loss_of(fb, step)
+        lb.backward()
+        if gather == "f16":
+            for p, f in zip(pb, fb):
+                p.grad.copy_(f.grad)
+        opt.step()
+        if gather == "f16":  # the gathered f16 copies equal the replicated path's f16 params
+            for p, q in zip(pa, pb):
+                assert torch.allclose(q._anr_shadow.float(), p.detach().half().float(),
+                                      rtol=2e-3, atol=1e-6)
+    opt.consolidate()
+    out[rank] = ([p.detach().clone() for p in pa], [p.detach().clone() for p in pb],
+                 opt.state_numel(), sum(sizes))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,gather", [(2, "f32"), (2, "f16"), (8, "f32"), (8, "f16")])
+def test_sharded_adam_matches_all_reduce_path(world, gather):
+    """ShardedAdam (reduce-scatter, AdamW on 1/W of the parameters, all-gather) against the
+    all-reduce + replicated AdamW path after 4 steps, at world sizes 2 and 8 (gloo):
+    parameters equal on every rank (to the f32 summation-order noise of the two
+    collectives), optimizer state 2n/W per rank."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sharded_worker, args=(world, _free_port(), gather, out), nprocs=world, join=True)
+    ref = out[0][0]
+    for r in range(world):
+        pa, pb, state, n = out[r]
+        for a, b, c in zip(pa, pb, ref):
+            assert torch.equal(a, c)  # the replicated path: identical on every rank
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (r, (a - b).abs().max())
+        assert state == 2 * (-(-n // world))

@@ -25,6 +25,10 @@ and the same stratified draws on both sides.
   semantics="reference", composite / loss from oracle/ref_f16.py with torch's CUDA
   accumulation), at 64 and 1,024 samples per ray: color maps within 1e-2, loss 5e-3,
   gradients 1e-1 relative L2;
+* f16 gradient error anchored to tcnn semantics: per module, the relative L2 distance
+  to the f64-exact gradient of the same f16-rounded forward, for the GPU build
+  numerics, the GPU reference numerics and the oracle's reference semantics; the build's
+  must not exceed the reference's own;
 * PSNR against reference semantics: the pipeline in reference numerics, the pipeline in
   build numerics and the reference-semantics oracle train side by side for 64 AdamW
   steps (8 epochs, same batches and draws); PSNR at 0 / 8 / 16 / 32 / 64 iterations. The
@@ -257,6 +261,40 @@ def test_train_step_reference_numerics(scene, dev, n_samples, B):
     assert rec["loss_rel"] <= tol["loss"], rec
     for m in ref_ingp.MODULES:
         assert rec["grad_" + m] <= tol["grad"], (m, rec)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n_samples,B", [(N, 200), (1024, 24)])
+def test_f16_gradient_error_vs_tcnn_semantics(scene, dev, n_samples, B):
+    """Per-module relative L2 error of the f16 gradients against the f64-exact gradient
+    of the same f16-rounded forward (oracle half=True, composite and backward in f64),
+    for the GPU's build numerics, the GPU's reference numerics, and the oracle's
+    reference semantics (what tcnn + the reference's f16 autograd compute). The build's
+    f16 backward (f32 between kernels, per-wavefront gradient scale) must be no less
+    accurate than the reference's own f16 gradients for every module."""
+    from atmonr_amd.batch_loader import BatchLoader
+
+    p, _ = _pair(scene, dev, torch.float16, n_samples=n_samples)
+    exact = _pair(scene, dev, None, None, n_samples, oracle_only=p, composite="f64")
+    pr, ref = _pair(scene, dev, torch.float16, n_samples=n_samples, numerics="reference")
+    batch = next(iter(BatchLoader(scene, B, seed=1)))
+    u = torch.rand(B, n_samples, generator=torch.Generator().manual_seed(2))
+    cb = ref_ingp.cpu_batch(batch)
+    for pipe in (p, pr):
+        pipe.compute_loss(batch, pipe.forward(batch, u=u.to(dev))).backward()
+    for o in (exact, ref):
+        o.loss(cb, o.forward(cb, u)).backward()
+    rec = {}
+    for m in ref_ingp.MODULES:
+        truth = exact.params[m].grad
+        rec[m] = {"gpu_build": _rel(getattr(p, m).params.grad.double().cpu(), truth),
+                  "gpu_reference_numerics": _rel(getattr(pr, m).params.grad.double().cpu(),
+                                                 truth),
+                  "oracle_reference_semantics": _rel(ref.params[m].grad, truth)}
+    _REC["f16_grad_error_vs_exact" + ("" if n_samples == N else f"_n{n_samples}")] = rec
+    _dump()
+    for m, r in rec.items():
+        assert r["gpu_build"] <= r["oracle_reference_semantics"] * 1.05 + 1e-6, (m, rec)
 
 
 class _ReferenceRunner:

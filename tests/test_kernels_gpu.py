@@ -555,6 +555,57 @@ def test_adam_multi_tensor_matches_torch_and_per_tensor(dev, decoupled):
             close(oa.state[x]["exp_avg_sq"], ob.state[z]["exp_avg_sq"], rel=1e-5, atol=1e-12)
 
 
+@pytest.mark.parametrize("multi", [True, False])
+def test_adam_groups_with_their_own_betas_eps(dev, multi):
+    """Param groups with different betas / eps each step with their own (as torch does):
+    one multi-tensor launch per (betas, eps) group."""
+    from atmonr_amd.optim import FusedAdam
+
+    gen = torch.Generator().manual_seed(5)
+    p0 = [torch.randn(n, generator=gen) for n in (513, 2049, 77)]
+    grads = [[torch.randn(x.numel(), generator=gen) * 0.1 for x in p0] for _ in range(3)]
+
+    def groups(ps):
+        return [{"params": ps[:1], "betas": (0.9, 0.99), "eps": 1e-15},
+                {"params": ps[1:2], "betas": (0.8, 0.9), "eps": 1e-8, "lr": 3e-3},
+                {"params": ps[2:], "betas": (0.95, 0.999), "eps": 1e-6, "weight_decay": 0.1}]
+
+    pa = [torch.nn.Parameter(x.clone().to(dev)) for x in p0]
+    pb = [torch.nn.Parameter(x.clone()) for x in p0]
+    oa = FusedAdam(groups(pa), lr=1e-2)
+    oa.multi_tensor = multi
+    ob = torch.optim.AdamW(groups(pb), lr=1e-2, foreach=False)
+    for gr in grads:
+        for x, z, g in zip(pa, pb, gr):
+            x.grad, z.grad = g.to(dev), g.clone()
+        oa.step()
+        ob.step()
+    for x, z in zip(pa, pb):
+        close(x.detach(), z.detach(), rel=1e-5, atol=1e-6)
+
+
+def test_adam_multi_validates_every_tensor_before_launching(dev):
+    """A bad descriptor after the first 16 tensors leaves every parameter untouched."""
+    import ctypes
+
+    from atmonr_amd import _lib
+
+    ps = [torch.randn(64, device=dev) for _ in range(18)]
+    before = [p.clone() for p in ps]
+    st = [(torch.randn(64, device=dev), torch.zeros(64, device=dev), torch.zeros(64, device=dev))
+          for _ in ps]
+    ts = [_lib.AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), None, 64,
+                          1e-2, 0.0, 1) for p, (g, m, v) in zip(ps, st)]
+    ts[17].grad = None  # null gradient pointer in the second launch's batch
+    arr = (_lib.AdamTensor * len(ts))(*ts)
+    with pytest.raises(_lib.ANRError, match="tensor 17"):
+        _lib.call("anr_adam_step_multi", ctypes.addressof(arr), len(ts), 0.9, 0.99, 1e-15, 1, 0,
+                  _lib.stream(dev))
+    torch.cuda.synchronize()
+    for p, b in zip(ps, before):
+        assert torch.equal(p, b)
+
+
 # ------------------------------------------------------------------ fused dir encoding + MLP
 @pytest.mark.parametrize("width,half", [(64, True), (64, False), (32, True)])
 def test_ingp_dir_mlp_matches_unfused(dev, width, half):

@@ -16,12 +16,25 @@ from __future__ import annotations
 
 import collections
 import csv
+import hashlib
 import json
 import os
 import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "atmospheric-neural-rendering_amd", "csrc")
+# bench.py kernel tag prefix -> the source file that defines it (PMC entries carry its
+# sha1, and bench.py ignores an entry whose kernel source has changed since)
+SOURCES = {"hash": "hashgrid.hip", "field": "field_fused.hip", "composite": "composite.hip",
+           "sampler": "sampler.hip"}
+
+
+def source_sha1(tag: str) -> str | None:
+    f = SOURCES.get(tag.split("_")[0])
+    if f is None:
+        return None
+    return hashlib.sha1(open(os.path.join(CSRC, f), "rb").read()).hexdigest()
 
 # bench.py kernel tag -> substring of the mangled/demangled kernel name
 TAGS = {
@@ -102,6 +115,7 @@ def main(src: str, tag: str, key_suffix: str = "baseline:8192x1024"):
                    "write_kib": round(w, 1), "source": tag}
             if a:  # TCC_EA0_ATOMIC_sum: memory-side atomic requests (64-B segments)
                 ent["atomic_requests"] = round(a)
+            ent["kernel_source_sha1"] = source_sha1(t)
             pmc[f"{t}:{key_suffix}"] = ent
     json.dump(pmc, open(pmc_path, "w"), indent=1, sort_keys=True)
     open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")

@@ -17,8 +17,10 @@ from ._lib import call, ptr
 
 
 class FusedAdam(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=None,
                  decoupled: bool = True, zero_grad_in_step: bool = False, **unused):
+        if weight_decay is None:  # torch.optim.AdamW's default 1e-2, Adam's 0
+            weight_decay = 1e-2 if decoupled else 0.0
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.decoupled = decoupled

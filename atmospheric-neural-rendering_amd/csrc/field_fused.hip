@@ -408,6 +408,34 @@ struct FwdWeights {
   __device__ h8 D2(int i) const { return d2[i]; }
 };
 
+// The backward's W^T fragments (Net::oB*), read from the LDS copy into registers a layer
+// or more before their MFMAs (bwd_rt_kernel): a read issued right before its first use
+// parks the wave on lgkmcnt for the whole LDS latency, with no other wave on the SIMD to
+// cover it.
+template <int W, int NHD>
+struct BwdFrags {
+  using N = Net<W, NHD>;
+  h4 d2[N::NT], p1[N::NT];
+  h8 d1[NHD == 2 ? N::NT * N::KB : 1], d0[N::KB], p0[2 * N::KB];
+  __device__ void load_d2(const _Float16* pk, int lane) {
+#pragma unroll
+    for (int i = 0; i < N::NT; ++i) d2[i] = *reinterpret_cast<const h4*>(pk + N::oBD2 + i * N::F16 + lane * 4);
+  }
+  __device__ void load_rest(const _Float16* pk, int lane) {
+    auto ld = [&](int off) { return *reinterpret_cast<const h8*>(pk + off + lane * 8); };
+    if constexpr (NHD == 2) {
+#pragma unroll
+      for (int i = 0; i < N::NT * N::KB; ++i) d1[i] = ld(N::oBD1 + i * N::F32);
+    }
+#pragma unroll
+    for (int i = 0; i < N::KB; ++i) d0[i] = ld(N::oBD0 + i * N::F32);
+#pragma unroll
+    for (int i = 0; i < N::NT; ++i) p1[i] = *reinterpret_cast<const h4*>(pk + N::oBP1 + i * N::F16 + lane * 4);
+#pragma unroll
+    for (int i = 0; i < 2 * N::KB; ++i) p0[i] = ld(N::oBP0 + i * N::F32);
+  }
+};
+
 // The same fragments read from a packed copy in LDS (backward kernel).
 template <int W, int NHD>
 struct LdsWeights {
@@ -1158,6 +1186,33 @@ __device__ __forceinline__ h4 tr_b(h8 x, h8 sel) {
   return to_h4<BF>(mma32<BF>(x, sel, f4{0.0f, 0.0f, 0.0f, 0.0f}));
 }
 
+// The same transposes through a wave-private LDS image (LT): each lane stores its 4 (C
+// tile) or 8 (B-operand tile) 16-bit values as one row piece, and ds_read_b64_tr_b16 hands
+// lane (g, c) column c of rows 4g..4g+3 — the layout tr_c / tr_b produce, bit for bit,
+// without the MFMA, its two f32 -> 16-bit conversions and their result wait states.
+// C tile: 16 rows (samples) x 16 units, 32-B rows, 8-B piece c of row r at c ^ (r >> 2):
+// the b64 writes (32 banks) and the transposed reads (64 banks, 32-lane halves) are both
+// conflict-free. B tile: 16 rows x 32 slots, 64-B rows, 16-B piece c of row r at
+// c ^ (2 * ((r >> 2) & 1)), so a 32-lane half's transposed read covers 64 distinct banks.
+__device__ __forceinline__ void lt_put_c(_Float16* img, int g, int li, h4 v) {
+  *reinterpret_cast<h4*>(img + li * 16 + 4 * (g ^ (li >> 2))) = v;
+}
+__device__ __forceinline__ h4 lt_get_c(const _Float16* img, int g, int li) {
+  const _Float16* p = img + (4 * g + (li >> 2)) * 16 + 4 * ((li & 3) ^ g);
+  return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p)));
+}
+__device__ __forceinline__ void lt_put_b(_Float16* img, int g, int li, h8 v) {
+  *reinterpret_cast<h8*>(img + li * 32 + 8 * (g ^ ((li >> 1) & 2))) = v;
+}
+// slots 16kb .. 16kb+15 of the B tile, transposed (= tr_b(x, sel[kb]))
+__device__ __forceinline__ h4 lt_get_b(const _Float16* img, int kb, int g, int li) {
+  const int r = 4 * g + (li >> 2), p = li & 3;
+  const _Float16* q = img + r * 32 + 8 * ((2 * kb + (p >> 1)) ^ ((r >> 1) & 2)) + 4 * (p & 1);
+  return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(q)));
+}
+constexpr int kLtSlot = 256;     // f16 elements of one C-tile image (a B tile takes two)
+constexpr int kLtRegion = 16;    // slots of one layer's transposes (32-sample tiles)
+
 // REF (reference numerics, f16 only): the gradient scale is tcnn's fixed loss scale
 // (a.loss_scale = 128) instead of the per-wavefront power of two, the ReLU masks test the
 // f16-rounded outputs, and the gradients that cross tinycudann module boundaries in the
@@ -1165,13 +1220,19 @@ __device__ __forceinline__ h4 tr_b(h8 x, h8 sel) {
 // dir_encoder as f16(f16(g_scaled) / 128) (a subnormal-flushing f16 division) and is
 // rescaled for pos_mlp, and dL/denc is written as f16(f16(g_scaled) / 128)
 // (tinycudann/modules.py: input_grad / loss_scale, cast to the f16 input's dtype).
-template <int W, int NHD, bool FAST, bool ROWS, bool BF, bool REF = false>
+// LT: the dW operand transposes through LDS (lt_put_* / lt_get_*) instead of MFMAs.
+template <int W, int NHD, bool FAST, bool ROWS, bool BF, bool REF = false, bool LT = false>
 __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64_t tpw,
                                                      const float* wmax) {
   static_assert(!(REF && BF), "reference numerics are f16");
+  // MT 16-sample halves per tile, the dW contraction over NP pairs of them. (64-sample
+  // tiles, MT = 4, measured 6 % slower at the same 1 wave/SIMD: profiles/r03_field_bwd_ab.log)
+  constexpr int MT = 2, TR = 16 * MT, NP = MT / 2;
   using N = Net<W, NHD>;
   constexpr int NT = N::NT, KB = N::KB;
   __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
+  // 4 wavefronts x two alternating regions (consecutive layers' transposes may overlap)
+  __shared__ __attribute__((aligned(16))) _Float16 trs[LT ? 4 * 2 * kLtRegion * kLtSlot : 8];
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
   for (int e = threadIdx.x * 8; e < N::n_packed; e += blockDim.x * 8)
@@ -1180,16 +1241,37 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   // per-tile opaque copy of the fragment base: the weight fragments are re-read from LDS
   // each tile instead of being hoisted into registers
   const _Float16* wbt = wsm;
-  auto bfrag32 = [&](int off) { return *reinterpret_cast<const h8*>(wbt + off + lane * 8); };
-  auto bfrag16 = [&](int off) { return *reinterpret_cast<const h4*>(wbt + off + lane * 4); };
   TrConst<BF> tc;
   tc.init(lane);
+  _Float16* const trw = trs + (LT ? wave * 2 * kLtRegion * kLtSlot : 0);
+  // dW operand transposes; `slot` (region * kLtRegion + index) names the LDS image (LT)
+  auto trc = [&](int slot, h4 x) -> h4 {
+    if constexpr (LT) {
+      _Float16* img = trw + slot * kLtSlot;
+      lt_put_c(img, g, li, x);
+      return lt_get_c(img, g, li);
+    } else {
+      return tr_c<BF>(x, tc.id);
+    }
+  };
+  auto trb = [&](int slot, h8 x, h4& o0, h4& o1) {
+    if constexpr (LT) {
+      _Float16* img = trw + slot * kLtSlot;
+      lt_put_b(img, g, li, x);
+      o0 = lt_get_b(img, 0, g, li);
+      o1 = lt_get_b(img, 1, g, li);
+    } else {
+      o0 = tr_b<BF>(x, tc.sel[0]);
+      o1 = tr_b<BF>(x, tc.sel[1]);
+    }
+  };
+  constexpr int R0 = 0, R1 = kLtRegion;
 
-  const int64_t n_tiles = (a.M + 31) / 32;
+  const int64_t n_tiles = (a.M + TR - 1) / TR;
   const int64_t w_id = static_cast<int64_t>(blockIdx.x) * waves + wave;
   const int64_t t_begin = w_id * tpw;
   const int64_t t_end = t_begin + tpw < n_tiles ? t_begin + tpw : n_tiles;
-  const int64_t n_full = a.M / 32;
+  const int64_t n_full = a.M / TR;
 
   f4 dD2[NT], dD1[NHD == 2 ? NT * NT : 1], dD0[NT * 2], dP1[NT], dP0[NT * 2];
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1217,13 +1299,13 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   // f32 -> f16 -> f32 (the reference's f16 tensors between modules)
   auto r16 = [](float v) { return static_cast<float>(static_cast<_Float16>(v)); };
 
-  Rows cur[2];
-  RawRows nraw[2];
+  Rows cur[MT];
+  RawRows nraw[MT];
   const int64_t t_full_end = t_end < n_full ? t_end : n_full;
   if constexpr (FAST) {
     if (t_begin < t_full_end) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, t_begin * 32 + mt * 16 + li, g, nraw[mt]);
+      for (int mt = 0; mt < MT; ++mt) load_raw<ROWS>(a, t_begin * TR + mt * 16 + li, g, nraw[mt]);
     }
   }
   auto process = [&](auto full_c, int64_t tile) {
@@ -1239,37 +1321,40 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     // recompute's first stage) and the compiler copies the prefetch registers right after,
     // a third into the tile, with an s_waitcnt for the next tile's loads (1 wave/SIMD:
     // nothing hides it). 0.990 -> 0.967 ms on the bench shape (profiles/r02_field_bwd_keep.log).
-    float keep[8] = {};
+    float keep[4 * MT] = {};
     if constexpr (FAST && FULL) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         raw_to_rows(nraw[mt], g, cur[mt]);
-        keep[3 * mt] = nraw[mt].d0;
-        keep[3 * mt + 1] = nraw[mt].d1;
-        keep[3 * mt + 2] = nraw[mt].d2;
-        keep[6 + mt] = nraw[mt].ds;
+        keep[4 * mt] = nraw[mt].d0;
+        keep[4 * mt + 1] = nraw[mt].d1;
+        keep[4 * mt + 2] = nraw[mt].d2;
+        keep[4 * mt + 3] = nraw[mt].ds;
       }
       const int64_t tn = tile + 1 < t_full_end ? tile + 1 : tile;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, tn * 32 + mt * 16 + li, g, nraw[mt]);
+      for (int mt = 0; mt < MT; ++mt) load_raw<ROWS>(a, tn * TR + mt * 16 + li, g, nraw[mt]);
     } else {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_rows<ROWS>(a, tile * 32 + mt * 16 + li, g, true, cur[mt]);
+      for (int mt = 0; mt < MT; ++mt) load_rows<ROWS>(a, tile * TR + mt * 16 + li, g, true, cur[mt]);
     }
     const bool full = FULL;
     // ---- forward recompute of both 16-sample halves; every activation stays in registers
-    Tile<W, NHD> t[2];
-    h4 gc[2];
-    bool dens[2];
+    Tile<W, NHD> t[MT];
+    h4 gc[MT];
+    bool dens[MT];
+    BwdFrags<W, NHD> bw;
     {
-      bool valid[2];
+      bool valid[MT];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) valid[mt] = full || tile * 32 + mt * 16 + li < a.M;
+      for (int mt = 0; mt < MT; ++mt) valid[mt] = full || tile * TR + mt * 16 + li < a.M;
       FwdWeights<W, NHD> fwl;
       fwl.load(wbt, lane);
-      tile_forward<W, NHD, 2, BF>(fwl, cur, valid, g, t, NoSink{});
+      bw.load_d2(wbt, lane);
+      tile_forward<W, NHD, MT, BF>(fwl, cur, valid, g, t, NoSink{});
+      bw.load_rest(wbt, lane);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         dens[mt] = (REF ? r16(t[mt].po[0]) : t[mt].po[0]) > 0.0f;
         f4 gv;
 #pragma unroll
@@ -1280,68 +1365,87 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     }
     auto last = [&](int mt, int kt) -> h4 { return NHD == 2 ? t[mt].hd1[kt] : t[mt].hd0[kt]; };
     // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
-    h4 dl[2][NT];
+    h4 dl[MT][NT];
     {
-      const h8 ga = cat(tr_c<BF>(gc[0], tc.id), tr_c<BF>(gc[1], tc.id));
+      h8 ga[NP];
+#pragma unroll
+      for (int pr = 0; pr < NP; ++pr)
+        ga[pr] = cat(trc(R0 + 0, gc[2 * pr]), trc(R0 + 1, gc[2 * pr + 1]));
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
-        const h8 xl = cat(tr_c<BF>(last(0, kt), tc.id), tr_c<BF>(last(1, kt), tc.id));
-        mma32_acc_v<BF>(dD2[kt], ga, xl);
-        const h4 wf = bfrag16(N::oBD2 + kt * N::F16);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) dl[mt][kt] = mask_h4<BF>(mma16<BF>(wf, gc[mt], z4), last(mt, kt));
+        for (int pr = 0; pr < NP; ++pr) {
+          const h8 xl = cat(trc(R0 + 2 + 2 * kt, last(2 * pr, kt)), trc(R0 + 3 + 2 * kt, last(2 * pr + 1, kt)));
+          mma32_acc_v<BF>(dD2[kt], ga[pr], xl);
+        }
+        const h4 wf = bw.d2[kt];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) dl[mt][kt] = mask_h4<BF>(mma16<BF>(wf, gc[mt], z4), last(mt, kt));
       }
     }
     // ---- dir hidden layer 1 (NHD == 2): dW_D1 (W x W) += dl^T · X_d0 ; dh0 = D1^T dl
-    h4 dh0[2][NT];
+    h4 dh0[MT][NT];
     if constexpr (NHD == 2) {
-      h8 gb[NT];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) gb[nt] = cat(tr_c<BF>(dl[0][nt], tc.id), tr_c<BF>(dl[1][nt], tc.id));
+      for (int pr = 0; pr < NP; ++pr) {
+        h8 gb[NT];
 #pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-        const h8 xb = cat(tr_c<BF>(t[0].hd0[kt], tc.id), tr_c<BF>(t[1].hd0[kt], tc.id));
+        for (int nt = 0; nt < NT; ++nt)
+          gb[nt] = cat(trc(R1 + 2 * nt, dl[2 * pr][nt]), trc(R1 + 1 + 2 * nt, dl[2 * pr + 1][nt]));
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) mma32_acc_v<BF>(dD1[nt * NT + kt], gb[nt], xb);
+        for (int kt = 0; kt < NT; ++kt) {
+          const h8 xb = cat(trc(R1 + 8 + 2 * kt, t[2 * pr].hd0[kt]), trc(R1 + 9 + 2 * kt, t[2 * pr + 1].hd0[kt]));
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) mma32_acc_v<BF>(dD1[nt * NT + kt], gb[nt], xb);
+        }
       }
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
-        f4 acc[2] = {z4, z4};
+        f4 acc[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-          const h8 wf = bfrag32(N::oBD1 + (kt * KB + kb) * N::F32);
+          const h8 wf = bw.d1[kt * KB + kb];
 #pragma unroll
-          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf, cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = mma32<BF>(wf, cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
         }
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) dh0[mt][kt] = mask_h4<BF>(acc[mt], t[mt].hd0[kt]);
+        for (int mt = 0; mt < MT; ++mt) dh0[mt][kt] = mask_h4<BF>(acc[mt], t[mt].hd0[kt]);
       }
     } else {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) dh0[mt][kt] = dl[mt][kt];
     }
     // ---- dir input layer: dW_D0 (W x 32, k' order) += dh0^T · X_de ; dpos = D0^T dh0
-    h4 dpo[2];
+    h4 dpo[MT];
     {
-      const h8 x0 = cat(tr_b<BF>(t[0].xd, tc.sel[0]), tr_b<BF>(t[1].xd, tc.sel[0]));
-      const h8 x1 = cat(tr_b<BF>(t[0].xd, tc.sel[1]), tr_b<BF>(t[1].xd, tc.sel[1]));
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const h8 gd = cat(tr_c<BF>(dh0[0][nt], tc.id), tr_c<BF>(dh0[1][nt], tc.id));
-        mma32_acc_v<BF>(dD0[nt * 2], gd, x0);
-        mma32_acc_v<BF>(dD0[nt * 2 + 1], gd, x1);
+      for (int pr = 0; pr < NP; ++pr) {
+        h4 a0, a1, b0, b1;
+        trb(R0 + 0, t[2 * pr].xd, a0, a1);
+        trb(R0 + 2, t[2 * pr + 1].xd, b0, b1);
+        const h8 x0 = cat(a0, b0), x1 = cat(a1, b1);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const h8 gd = cat(trc(R0 + 4 + 2 * nt, dh0[2 * pr][nt]), trc(R0 + 5 + 2 * nt, dh0[2 * pr + 1][nt]));
+          mma32_acc_v<BF>(dD0[nt * 2], gd, x0);
+          mma32_acc_v<BF>(dD0[nt * 2 + 1], gd, x1);
+        }
       }
-      f4 acc[2] = {z4, z4};
+      f4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        const h8 wf = bfrag32(N::oBD0 + kb * N::F32);
+        const h8 wf = bw.d0[kb];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf, cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mma32<BF>(wf, cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
       }
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         if constexpr (REF) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc[mt][i] = r16(r16(r16(acc[mt][i]) * inv_s) * s);
@@ -1353,40 +1457,53 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       }
     }
     // ---- pos output layer: dW_P1 (16 x W) += dpo^T · X_ph ; dhp = P1^T dpo
-    h4 dhp[2][NT];
+    h4 dhp[MT][NT];
     {
-      const h8 ga = cat(tr_c<BF>(dpo[0], tc.id), tr_c<BF>(dpo[1], tc.id));
+      h8 ga[NP];
+#pragma unroll
+      for (int pr = 0; pr < NP; ++pr)
+        ga[pr] = cat(trc(R1 + 0, dpo[2 * pr]), trc(R1 + 1, dpo[2 * pr + 1]));
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
-        const h8 xp = cat(tr_c<BF>(t[0].hp[kt], tc.id), tr_c<BF>(t[1].hp[kt], tc.id));
-        mma32_acc_v<BF>(dP1[kt], ga, xp);
-        const h4 wf = bfrag16(N::oBP1 + kt * N::F16);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) dhp[mt][kt] = mask_h4<BF>(mma16<BF>(wf, dpo[mt], z4), t[mt].hp[kt]);
+        for (int pr = 0; pr < NP; ++pr) {
+          const h8 xp = cat(trc(R1 + 2 + 2 * kt, t[2 * pr].hp[kt]), trc(R1 + 3 + 2 * kt, t[2 * pr + 1].hp[kt]));
+          mma32_acc_v<BF>(dP1[kt], ga[pr], xp);
+        }
+        const h4 wf = bw.p1[kt];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) dhp[mt][kt] = mask_h4<BF>(mma16<BF>(wf, dpo[mt], z4), t[mt].hp[kt]);
       }
     }
     // ---- pos input layer: dW_P0 (W x 32) += dhp^T · X_pe ; d_enc = P0^T dhp
     {
-      const h8 x0 = cat(tr_b<BF>(t[0].xe, tc.sel[0]), tr_b<BF>(t[1].xe, tc.sel[0]));
-      const h8 x1 = cat(tr_b<BF>(t[0].xe, tc.sel[1]), tr_b<BF>(t[1].xe, tc.sel[1]));
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const h8 gp = cat(tr_c<BF>(dhp[0][nt], tc.id), tr_c<BF>(dhp[1][nt], tc.id));
-        mma32_acc_v<BF>(dP0[nt * 2], gp, x0);
-        mma32_acc_v<BF>(dP0[nt * 2 + 1], gp, x1);
+      for (int pr = 0; pr < NP; ++pr) {
+        h4 a0, a1, b0, b1;
+        trb(R0 + 0, t[2 * pr].xe, a0, a1);
+        trb(R0 + 2, t[2 * pr + 1].xe, b0, b1);
+        const h8 x0 = cat(a0, b0), x1 = cat(a1, b1);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const h8 gp = cat(trc(R0 + 4 + 2 * nt, dhp[2 * pr][nt]), trc(R0 + 5 + 2 * nt, dhp[2 * pr + 1][nt]));
+          mma32_acc_v<BF>(dP0[nt * 2], gp, x0);
+          mma32_acc_v<BF>(dP0[nt * 2 + 1], gp, x1);
+        }
       }
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        f4 acc[2] = {z4, z4};
+        f4 acc[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-          const h8 wf = bfrag32(N::oBP0 + (kt * KB + kb) * N::F32);
+          const h8 wf = bw.p0[kt * KB + kb];
 #pragma unroll
-          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf, cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = mma32<BF>(wf, cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
         }
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int64_t row = tile * 32 + mt * 16 + li;
+        for (int mt = 0; mt < MT; ++mt) {
+          const int64_t row = tile * TR + mt * 16 + li;
           if (full || row < a.M) {
             f4 v = acc[mt] * inv_s;
             if constexpr (REF) {
@@ -1398,9 +1515,11 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         }
       }
     }
-    if constexpr (FAST && FULL)
-      asm volatile("" ::"v"(keep[0]), "v"(keep[1]), "v"(keep[2]), "v"(keep[3]), "v"(keep[4]),
-                   "v"(keep[5]), "v"(keep[6]), "v"(keep[7]));
+    if constexpr (FAST && FULL) {
+#pragma unroll
+      for (int i = 0; i < 4 * MT; i += 4)
+        asm volatile("" ::"v"(keep[i]), "v"(keep[i + 1]), "v"(keep[i + 2]), "v"(keep[i + 3]));
+    }
     // the last dW MFMAs of the tile have written their accumulators before anything
     // (a loop-exit copy) reads them
     agpr_fence();
@@ -1450,7 +1569,8 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
 // ---------------------------------------------------------------------------------
 static int g_target_log2 = 6;  // f16 gradient scale: max |dL/dout| of a wavefront -> 2^6
 // backward kernel generation: 0 = LDS tiles (bwd_kernel), 1 = register-transposed
-// (bwd_rt_kernel); test / A-B hook anr_ingp_field_force_bwd
+// (bwd_rt_kernel, MFMA transposes), 2 = the same with the transposes through LDS (LT);
+// test / A-B hook anr_ingp_field_force_bwd
 static int g_bwd_mode = 1;
 // forward form: 1 = the uniform-tile kernel where the shapes allow (default), 0 = always
 // the general kernel; test / A-B hook anr_ingp_field_force_fwd
@@ -1467,13 +1587,16 @@ static const void* bwd_fn(bool fast, int mode) {
   if (mode == 1)
     return fast ? reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, true, false, BF>)
                 : reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, false, false, BF>);
+  if (mode == 2)
+    return fast ? reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, true, false, BF, false, true>)
+                : reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, false, false, BF, false, true>);
   return fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true, false, BF>)
               : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false, false, BF>);
 }
 template <int W, int NHD, bool BF>
 static BwdGeom bwd_geom(int64_t M, bool fast, int mode) {
   const int waves = 4;
-  static int pc[2][2] = {{0, 0}, {0, 0}};
+  static int pc[3][2] = {{0, 0}, {0, 0}, {0, 0}};
   int& p = pc[mode][fast ? 1 : 0];
   if (p == 0) {
     int nb = 0;
@@ -1494,7 +1617,7 @@ static int64_t bwd_workspace(int64_t M) {
   // the largest wave count of the backward kernels (both generations, fast and general
   // d_color layouts), so a workspace sized once serves whichever runs
   int64_t n = 0;
-  for (int mode = 0; mode < 2; ++mode)
+  for (int mode = 0; mode < 3; ++mode)
     for (int f = 0; f < 2; ++f) {
       const int64_t w = bwd_geom<W, NHD, BF>(M, f == 1, mode).nw;
       n = w > n ? w : n;
@@ -1551,7 +1674,8 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
     }
   }
   const int mode = g_bwd_mode;
-  const size_t lds = (static_cast<size_t>(N::n_packed) + (mode == 1 ? 0 : waves * N::wave_lds)) * 2;
+  const size_t lds = (static_cast<size_t>(N::n_packed) + (mode == 0 ? waves * N::wave_lds : 0) +
+                      (mode == 2 ? 4 * 2 * kLtRegion * kLtSlot : 0)) * 2;
   if (lds > 160 * 1024) return 1;
   const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast, mode);
   if (!BF && (ws == nullptr || ws_bytes < static_cast<int64_t>(sizeof(float)) * gm.nw)) return 2;
@@ -1565,7 +1689,16 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
   }
 #define ANR_BWD_LAUNCH(K, FASTV, ROWSV) \
   hipLaunchKernelGGL((K<W, NHD, FASTV, ROWSV, BF>), grid, block, 0, st, a, target, gm.tpw, ws)
-  if (mode == 1) {
+#define ANR_BWD_LAUNCH_LT(FASTV, ROWSV)                                                        \
+  hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, FASTV, ROWSV, BF, false, true>), grid, block, 0, st, \
+                     a, target, gm.tpw, ws)
+  if (mode == 2) {
+    if (a.rows) {
+      if (fast) ANR_BWD_LAUNCH_LT(true, true); else ANR_BWD_LAUNCH_LT(false, true);
+    } else {
+      if (fast) ANR_BWD_LAUNCH_LT(true, false); else ANR_BWD_LAUNCH_LT(false, false);
+    }
+  } else if (mode == 1) {
     if (a.rows) {
       if (fast) ANR_BWD_LAUNCH(bwd_rt_kernel, true, true); else ANR_BWD_LAUNCH(bwd_rt_kernel, false, true);
     } else {
@@ -1579,6 +1712,7 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
     }
   }
 #undef ANR_BWD_LAUNCH
+#undef ANR_BWD_LAUNCH_LT
   return 0;
 }
 
@@ -1657,7 +1791,7 @@ extern "C" int64_t anr_ingp_field_bwd_workspace_bytes(const anr_mlp_desc* pos,
 
 extern "C" int anr_ingp_field_force_bwd(int32_t mode) {
   const int prev = g_bwd_mode;
-  if (mode == 0 || mode == 1) g_bwd_mode = mode;
+  if (mode >= 0 && mode <= 2) g_bwd_mode = mode;
   return prev;
 }
 

@@ -315,9 +315,10 @@ def main():
                          "gradient, AdamW on 1/N of the parameters, all-gather of the f16 "
                          "compute copy (f16) or of the f32 parameters (f32), instead of "
                          "all-reduce + replicated AdamW")
-    ap.add_argument("--field-bwd", choices=["rt", "lds"], default="rt",
+    ap.add_argument("--field-bwd", choices=["rt", "rt_lt", "lds"], default="rt",
                     help="fused field backward generation (anr_ingp_field_force_bwd): "
-                         "register-transposed (default) or LDS-staged tiles")
+                         "register-transposed (default), the same with the dW operand "
+                         "transposes through LDS, or LDS-staged tiles")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every kernel timed (per-kernel breakdown)")
     args = ap.parse_args()
@@ -351,7 +352,7 @@ def main():
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
     from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
 
-    _lib.load().anr_ingp_field_force_bwd(1 if args.field_bwd == "rt" else 0)
+    _lib.load().anr_ingp_field_force_bwd({"lds": 0, "rt": 1, "rt_lt": 2}[args.field_bwd])
     t0 = time.time()
     ds = SyntheticHARP2Dataset(n_views=args.views, img_size=args.img_size, device=dev, seed=0)
     torch.cuda.synchronize()

@@ -270,8 +270,9 @@ int64_t anr_ingp_field_packed_size(const anr_mlp_desc* pos, const anr_mlp_desc* 
 int anr_ingp_field_set_grad_scale(int32_t log2_target);
 /* Backward kernel generation: 0 = layer inputs and gradient tiles staged in LDS, 1 =
  * register-transposed (default; transposes by MFMA against a 0/1 matrix, LDS holds only
- * the weights). Same math and results. Test / A-B hook; process-wide; other values keep
- * the current mode. Returns the previous mode. */
+ * the weights), 2 = register-transposed with the dW operand transposes through LDS
+ * (ds_read_b64_tr_b16). Same math; bit-identical dL/denc. Test / A-B hook; process-wide;
+ * other values keep the current mode. Returns the previous mode. */
 int anr_ingp_field_force_bwd(int32_t mode);
 /* Forward kernel form: 1 = the uniform-tile form wherever the shapes allow it (default:
  * dense rows, samples_per_ray a multiple of 16, 4 colour outputs, 16-byte aligned colour

@@ -209,7 +209,9 @@ class RefInstantNGP:
             off += o * i
             h = h @ W.t()
             if k < len(shapes) - 1:
-                h = _RoundBoth.apply(torch.relu(h))
+                # f16 tile: relu, rounded value and gradient, mask on the stored f16
+                # activation (tcnn's ReLU backward)
+                h = ref_tcnn.ReluRound.apply(h, torch.float16, True)
         return h[:, :n_out]
 
     def _grid_ref(self, cfg):

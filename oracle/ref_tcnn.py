@@ -161,11 +161,42 @@ class _RoundValue(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, dtype):
-        return x.to(dtype).to(x.dtype)
+        return x.to(dtype).double()
 
     @staticmethod
     def backward(ctx, g):
         return g, None
+
+
+class ReluRound(torch.autograd.Function):
+    """relu(x) rounded to ``dtype`` (a hidden activation of an f16 / bf16 MLP tile). The
+    backward masks with the ROUNDED output, as tcnn's ReLU backward tests the stored f16
+    activation > 0 (so a pre-activation below the f16 subnormal range passes no
+    gradient); ``round_grad`` also rounds the gradient to ``dtype`` (tcnn's f16 gradient
+    tiles, reference semantics), else it passes in full precision."""
+
+    @staticmethod
+    def forward(ctx, x, dtype, round_grad):
+        y = torch.relu(x).to(dtype).to(x.dtype)
+        ctx.save_for_backward(y)
+        ctx.dtype, ctx.round_grad = dtype, round_grad
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        g = torch.where(y > 0, g, torch.zeros_like(g))
+        if ctx.round_grad:
+            g = g.to(ctx.dtype).to(y.dtype)
+        return g, None, None
+
+
+def relu_rounder(half, round_grad: bool = False):
+    """Hidden-layer ReLU + rounding of an MLP tile: identity rounding for half=False."""
+    if not half:
+        return torch.relu
+    dt = torch.bfloat16 if half == "bf16" else torch.float16
+    return lambda t: ReluRound.apply(t, dt, round_grad)
 
 
 def rounder(half):
@@ -189,12 +220,13 @@ def mlp_fwd(x: torch.Tensor, params: torch.Tensor, n_in, n_out, width, n_hidden,
     h = torch.ones(x.shape[0], nip, dtype=torch.float64)
     h = torch.cat([rnd(x.double()), h[:, n_in:]], dim=1)
     off = 0
+    act = relu_rounder(half)
     for k, (o, i) in enumerate(shapes):
         W = rnd(params[off:off + o * i].double()).view(o, i)
         off += o * i
         h = h @ W.t()
-        if k < len(shapes) - 1 or output_relu:
-            h = torch.relu(h)
         if k < len(shapes) - 1:
-            h = rnd(h)
+            h = act(h)  # relu, rounded; backward masks on the rounded activation
+        elif output_relu:
+            h = torch.relu(h)
     return h[:, :n_out]

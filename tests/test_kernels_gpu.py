@@ -695,12 +695,16 @@ def _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd, half=True):
 
 
 # field backward generations (anr_ingp_field_force_bwd): "rt" = register-transposed
-# (default), "lds" = layer inputs / gradient tiles staged in LDS
-@pytest.fixture(params=["rt", "lds"])
+# (default), "rt_lt" = the same with the dW operand transposes through LDS, "lds" =
+# layer inputs / gradient tiles staged in LDS
+_BWD_MODES = {"lds": 0, "rt": 1, "rt_lt": 2}
+
+
+@pytest.fixture(params=["rt", "rt_lt", "lds"])
 def field_bwd_mode(request):
     from atmonr_amd import _lib
 
-    prev = _lib.load().anr_ingp_field_force_bwd(1 if request.param == "rt" else 0)
+    prev = _lib.load().anr_ingp_field_force_bwd(_BWD_MODES[request.param])
     yield request.param
     _lib.load().anr_ingp_field_force_bwd(prev)
 
@@ -810,11 +814,12 @@ def test_ingp_field_unsupported_and_empty(dev):
 @pytest.mark.parametrize("mma", ["f16", "bf16"])
 @pytest.mark.parametrize("width,nhd", [(64, 2), (32, 1)])
 def test_ingp_field_bwd_generations_agree(dev, width, nhd, mma):
-    """The register-transposed backward (mode 1) and the LDS-tile backward (mode 0) on the
-    same inputs (256 rays x 1024 samples plus a ragged 77-row tail): d_enc bit-identical
-    (the dX chain is the same MFMA sequence on the same operands; the transposes are
-    exact), parameter gradients within 1e-5 relative L2 (the dW contraction visits the
-    32 samples of a tile in a different K order, and the flush is atomic)."""
+    """The register-transposed backward (mode 1), the same with LDS transposes (mode 2) and
+    the LDS-tile backward (mode 0) on the same inputs (256 rays x 1024 samples plus a
+    ragged 77-row tail): d_enc bit-identical (the dX chain is the same MFMA sequence on the
+    same operands; the transposes are exact), parameter gradients within 1e-5 relative L2
+    (mode 0's dW contraction visits the 32 samples of a tile in a different K order, and
+    the flush is atomic)."""
     from atmonr_amd import _lib
 
     nb, R, n_per_ray = 4, 256, 1024
@@ -837,7 +842,7 @@ def test_ingp_field_bwd_generations_agree(dev, width, nhd, mma):
     ws_bytes = lib.anr_ingp_field_bwd_workspace_bytes(pb, db, code, M)
     ws = torch.empty(max(1, ws_bytes // 4), device=dev)
     out = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         prev = lib.anr_ingp_field_force_bwd(mode)
         try:
             d_enc = torch.full((M, 32), float("nan"), device=dev)
@@ -850,10 +855,11 @@ def test_ingp_field_bwd_generations_agree(dev, width, nhd, mma):
         finally:
             lib.anr_ingp_field_force_bwd(prev)
         out[mode] = (d_enc, g_pos, g_dir)
-    assert torch.equal(out[0][0], out[1][0])
-    for i in (1, 2):
-        a, b = out[1][i], out[0][i]
-        assert ((a - b).norm() / b.norm()).item() <= 1e-5
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    for m in (0, 2):
+        assert torch.equal(out[m][0], out[1][0]), m
+        for i in (1, 2):
+            assert rel(out[m][i], out[1][i]) <= 1e-5, (m, i)
 
 
 @pytest.mark.gpu

@@ -76,6 +76,25 @@ def main():
         out["d_enc_rel_l2_per_level"] = [
             ((ge_[:, 2 * l:2 * l + 2] - go[:, 2 * l:2 * l + 2]).norm()
              / go[:, 2 * l:2 * l + 2].norm().clamp_min(1e-300)).item() for l in range(16)]
+    if "enc" in captured:
+        # which samples differ, and how close their pos-MLP pre-activations are to 0
+        rows = torch.nonzero((ge_ != go).any(1)).view(-1)
+        out["rows_differing"] = int(rows.numel())
+        enc = captured["enc"].detach().double()
+        W0 = o.params["pos_mlp"].detach()[:64 * 32].half().double().view(64, 32)
+        W1 = o.params["pos_mlp"].detach()[64 * 32:].half().double().view(16, 64)
+        pre = enc @ W0.t()
+        hid = torch.relu(pre).half().double()
+        po = hid @ W1.t()
+        absmin = pre.abs().min(1).values
+        out["rows_differing_sample_pos"] = (rows % N).tolist()[:64]
+        out["rows_differing_min_abs_preact"] = absmin[rows].tolist()[:32]
+        out["all_rows_min_abs_preact_median"] = absmin.median().item()
+        out["rows_differing_pos_out0"] = po[rows, 0].tolist()[:32]
+        rel = ((ge_ - go).abs().max(1).values / go.abs().max(1).values.clamp_min(1e-30))[rows]
+        out["rows_differing_rel_maxdiff"] = rel.tolist()[:32]
+        out["rows_differing_d_enc_gpu_norm"] = ge_[rows].norm(dim=1).tolist()[:16]
+        out["rows_differing_d_enc_oracle_norm"] = go[rows].norm(dim=1).tolist()[:16]
     # table gradient level by level
     offs, sizes, res_, scales, _ = ref_tcnn.grid_levels(3, 16, 16, 1.3819, 19)
     gg = p.pos_encoder.params.grad.double().cpu()

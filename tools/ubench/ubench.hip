@@ -10,6 +10,10 @@
 //               segment-aligned address of a `n_floats` table -> segment requests/s.
 //               seg_lanes = 4 with 16 segments per instruction is the hash-grid
 //               backward's shape (hashgrid.hip v2: lane = 4*level + 2*xbit + feature).
+//   ub_gather   4-B loads (one f16x2 hash-grid corner, the forward's gather width) at
+//               independent random addresses of an `n_words` table, `iters` per lane ->
+//               a known count of requested bytes, to calibrate rocprofv3 FETCH_SIZE and
+//               the TCC hit rate for this access shape.
 //
 // Test/measurement infrastructure, not product: built to tools/ubench/libanr_ubench.so
 // by __graft_entry__.build(); bench.py loads it in its untimed phase. Plain C ABI
@@ -120,6 +124,20 @@ __global__ void __launch_bounds__(256) atomic_kernel(float* __restrict__ table, 
   }
 }
 
+__global__ void __launch_bounds__(256) gather_kernel(const uint32_t* __restrict__ table,
+                                                     int64_t n_words, int iters, uint32_t seed,
+                                                     uint32_t* __restrict__ sink) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+#pragma unroll 8
+  for (int i = 0; i < iters; ++i) {
+    const uint32_t h = mix32(seed ^ mix32(gid * 0x9E3779B9U + (uint32_t)i * 0x85EBCA6BU));
+    const int64_t w = (int64_t)(((uint64_t)h * (uint64_t)n_words) >> 32);
+    acc ^= table[w];
+  }
+  if (acc == 0x12345678u) sink[gid & 255] = acc;  // keeps the loads; never true here
+}
+
 extern "C" {
 
 int ub_copy(const void* src, void* dst, int64_t n_float4, int blocks, void* stream) {
@@ -155,6 +173,15 @@ int ub_atomic(float* table, int64_t n_floats, int seg_lanes, int iters, int bloc
     return 1;
   atomic_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(table, n_floats / seg_lanes, seg_lanes,
                                                          iters, seed);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Gathers = blocks * 256 * iters, 4 B each.
+int ub_gather(const void* table, int64_t n_words, int iters, int blocks, uint32_t seed,
+              void* sink, void* stream) {
+  if (n_words <= 0 || iters <= 0 || blocks <= 0) return 1;
+  gather_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((const uint32_t*)table, n_words, iters,
+                                                         seed, (uint32_t*)sink);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

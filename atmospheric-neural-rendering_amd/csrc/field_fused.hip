@@ -316,19 +316,22 @@ __device__ __forceinline__ h8 enc_in(h8 e) {
 }
 // ReLU derivative: keep g where the forward activation (>= 0, f16) is nonzero. On the bits:
 // v_pk_min_u16(act, 1) is 0 or 1 per half and v_pk_mul_lo_u16 by it keeps or clears g
-// (two instructions per pair; written as asm because the compiler expands it to selects).
-__device__ __forceinline__ uint32_t mask2(uint32_t g, uint32_t act) {
-  uint32_t m, r;
-  // op_sel_hi:[1,0]: the high half of the constant operand also reads its low 16 bits (= 1)
-  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(m) : "v"(act));
-  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(g), "v"(m));
-  return r;
-}
+// (two instructions per pair; written as asm because the compiler expands it to compares
+// and selects). The result feeds MFMAs, and hipcc pads nothing for a VALU write inside an
+// asm statement: the two wait states a VALU-written MFMA operand needs end the string.
 template <bool BF>
 __device__ __forceinline__ h4 mask_h4(f4 g, h4 act) {
   typedef uint32_t u2 __attribute__((ext_vector_type(2)));
   const u2 gb = __builtin_bit_cast(u2, to_h4<BF>(g)), ab = __builtin_bit_cast(u2, act);
-  return __builtin_bit_cast(h4, u2{mask2(gb.x, ab.x), mask2(gb.y, ab.y)});
+  uint32_t m0, m1;
+  asm("v_pk_min_u16 %0, %2, 1 op_sel_hi:[1,0]\n\t"
+      "v_pk_min_u16 %1, %3, 1 op_sel_hi:[1,0]\n\t"
+      "v_pk_mul_lo_u16 %0, %4, %0\n\t"
+      "v_pk_mul_lo_u16 %1, %5, %1\n\t"
+      "s_nop 1"
+      : "=&v"(m0), "=&v"(m1)
+      : "v"(ab.x), "v"(ab.y), "v"(gb.x), "v"(gb.y));
+  return __builtin_bit_cast(h4, u2{m0, m1});
 }
 
 // Global inputs of one 16-sample half-tile for this lane, loaded a tile ahead.
@@ -370,16 +373,24 @@ __device__ __forceinline__ void load_rows(const Args& a, int64_t row, int g, boo
 }
 
 // Input row of the dir MLP for the sample in this lane (B-operand slots 8g..8g+7).
+// Branch-free (per-lane selects): a divergent branch here gives the compiler a place to
+// merge other g == 0 code into, including uses of the backward's prefetched loads, which
+// then wait for those loads at once.
 template <bool BF>
 __device__ __forceinline__ h8 dir_input(const Rows& in, bool valid, int g, f4 po) {
-  if (!valid) return h8{};
-  if (g == 0)
-    return h8{cvt1<BF>(1.0f), cvt1<BF>(po[1]), cvt1<BF>(po[2]), cvt1<BF>(po[3]),
-              cvt1<BF>(0.28209479177387814f), cvt1<BF>(-0.48860251190291987f * in.dy),
-              cvt1<BF>(0.48860251190291987f * in.dz), cvt1<BF>(-0.48860251190291987f * in.dx)};
   const _Float16 one = cvt1<BF>(1.0f);
-  return h8{cvt1<BF>(po[0]), cvt1<BF>(po[1]), cvt1<BF>(po[2]), cvt1<BF>(po[3]), one, one, one,
-            one};
+  const h8 lead = {one, cvt1<BF>(po[1]), cvt1<BF>(po[2]), cvt1<BF>(po[3]),
+                   cvt1<BF>(0.28209479177387814f), cvt1<BF>(-0.48860251190291987f * in.dy),
+                   cvt1<BF>(0.48860251190291987f * in.dz), cvt1<BF>(-0.48860251190291987f * in.dx)};
+  const h8 rest = {cvt1<BF>(po[0]), cvt1<BF>(po[1]), cvt1<BF>(po[2]), cvt1<BF>(po[3]), one, one,
+                   one, one};
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const u4 l = __builtin_bit_cast(u4, lead), r = __builtin_bit_cast(u4, rest);
+  const bool g0 = g == 0;
+  u4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = valid ? (g0 ? l[i] : r[i]) : 0u;
+  return __builtin_bit_cast(h8, v);
 }
 
 template <int W, int NHD>
@@ -406,34 +417,6 @@ struct FwdWeights {
   __device__ h8 D0(int i) const { return d0[i]; }
   __device__ h8 D1(int i) const { return d1[i]; }
   __device__ h8 D2(int i) const { return d2[i]; }
-};
-
-// The backward's W^T fragments (Net::oB*), read from the LDS copy into registers a layer
-// or more before their MFMAs (bwd_rt_kernel): a read issued right before its first use
-// parks the wave on lgkmcnt for the whole LDS latency, with no other wave on the SIMD to
-// cover it.
-template <int W, int NHD>
-struct BwdFrags {
-  using N = Net<W, NHD>;
-  h4 d2[N::NT], p1[N::NT];
-  h8 d1[NHD == 2 ? N::NT * N::KB : 1], d0[N::KB], p0[2 * N::KB];
-  __device__ void load_d2(const _Float16* pk, int lane) {
-#pragma unroll
-    for (int i = 0; i < N::NT; ++i) d2[i] = *reinterpret_cast<const h4*>(pk + N::oBD2 + i * N::F16 + lane * 4);
-  }
-  __device__ void load_rest(const _Float16* pk, int lane) {
-    auto ld = [&](int off) { return *reinterpret_cast<const h8*>(pk + off + lane * 8); };
-    if constexpr (NHD == 2) {
-#pragma unroll
-      for (int i = 0; i < N::NT * N::KB; ++i) d1[i] = ld(N::oBD1 + i * N::F32);
-    }
-#pragma unroll
-    for (int i = 0; i < N::KB; ++i) d0[i] = ld(N::oBD0 + i * N::F32);
-#pragma unroll
-    for (int i = 0; i < N::NT; ++i) p1[i] = *reinterpret_cast<const h4*>(pk + N::oBP1 + i * N::F16 + lane * 4);
-#pragma unroll
-    for (int i = 0; i < 2 * N::KB; ++i) p0[i] = ld(N::oBP0 + i * N::F32);
-  }
 };
 
 // The same fragments read from a packed copy in LDS (backward kernel).
@@ -1241,6 +1224,8 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   // per-tile opaque copy of the fragment base: the weight fragments are re-read from LDS
   // each tile instead of being hoisted into registers
   const _Float16* wbt = wsm;
+  auto bfrag32 = [&](int off) { return *reinterpret_cast<const h8*>(wbt + off + lane * 8); };
+  auto bfrag16 = [&](int off) { return *reinterpret_cast<const h4*>(wbt + off + lane * 4); };
   TrConst<BF> tc;
   tc.init(lane);
   _Float16* const trw = trs + (LT ? wave * 2 * kLtRegion * kLtSlot : 0);
@@ -1300,40 +1285,54 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   auto r16 = [](float v) { return static_cast<float>(static_cast<_Float16>(v)); };
 
   Rows cur[MT];
-  RawRows nraw[MT];
+  // the next tile's raw inputs, loaded a tile ahead into alternating register sets (the
+  // full-tile loop runs two tiles per trip): with one set, the loop-carried copy of the
+  // prefetch registers lands wherever the register allocator puts it, and where that is
+  // early in the tile it waits on the loads just issued (1 wave/SIMD: nothing hides it)
+  RawRows nr0[MT], nr1[MT];
   const int64_t t_full_end = t_end < n_full ? t_end : n_full;
   if constexpr (FAST) {
     if (t_begin < t_full_end) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) load_raw<ROWS>(a, t_begin * TR + mt * 16 + li, g, nraw[mt]);
+      for (int mt = 0; mt < MT; ++mt) load_raw<ROWS>(a, t_begin * TR + mt * 16 + li, g, nr0[mt]);
+      // drained once, so the loop entry carries no pending loads: entered with the first
+      // prefetch in flight, the waitcnt pass merges that state with the back edge's (the
+      // prefetch, then the tile's d_enc stores) into a wait for everything, stores
+      // included, at the head of every tile
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     }
   }
-  auto process = [&](auto full_c, int64_t tile) {
+  auto process = [&](auto full_c, int64_t tile, RawRows(&nraw)[MT], RawRows(&nnext)[MT]) {
     constexpr bool FULL = decltype(full_c)::value;
     {
       int zoff = 0;
       asm volatile("" : "+v"(zoff));
       wbt = wsm + zoff;
     }
-    // The previous tile's raw directions and dL/dsigma, kept live to the end of the tile:
-    // the loop-carried copies of the next tile's prefetched values then sit at the end of
-    // the iteration. Without it they die early (the direction remap is the forward
-    // recompute's first stage) and the compiler copies the prefetch registers right after,
-    // a third into the tile, with an s_waitcnt for the next tile's loads (1 wave/SIMD:
-    // nothing hides it). 0.990 -> 0.967 ms on the bench shape (profiles/r02_field_bwd_keep.log).
-    float keep[4 * MT] = {};
     if constexpr (FAST && FULL) {
+      // the tile's head: this tile's prefetched inputs are converted here (hoisted into the
+      // previous tile, the conversion waits on loads just issued) and the next tile's loads
+      // are issued here (the scheduler otherwise sinks them toward the tile's end)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        raw_to_rows(nraw[mt], g, cur[mt]);
-        keep[4 * mt] = nraw[mt].d0;
-        keep[4 * mt + 1] = nraw[mt].d1;
-        keep[4 * mt + 2] = nraw[mt].d2;
-        keep[4 * mt + 3] = nraw[mt].ds;
+        // ordered (volatile) uses of the prefetched registers: without them the select /
+        // remap of raw_to_rows floats up to the loads in the previous tile. The scalars
+        // are copied by a real v_mov, not an empty tied asm: the remap's packed FMA wants
+        // (d1, d2) in an aligned pair, and a tied operand would move that copy up to the
+        // dwordx3 load (where it waits for it)
+        RawRows rr = nraw[mt];
+        asm volatile("v_mov_b32 %0, %1" : "=v"(rr.d0) : "v"(nraw[mt].d0));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(rr.d1) : "v"(nraw[mt].d1));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(rr.d2) : "v"(nraw[mt].d2));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(rr.ds) : "v"(nraw[mt].ds));
+        asm volatile("" : "+v"(rr.dc));
+        raw_to_rows(rr, g, cur[mt]);
       }
       const int64_t tn = tile + 1 < t_full_end ? tile + 1 : tile;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) load_raw<ROWS>(a, tn * TR + mt * 16 + li, g, nraw[mt]);
+      for (int mt = 0; mt < MT; ++mt) load_raw<ROWS>(a, tn * TR + mt * 16 + li, g, nnext[mt]);
+      __builtin_amdgcn_sched_barrier(0);
     } else {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) load_rows<ROWS>(a, tile * TR + mt * 16 + li, g, true, cur[mt]);
@@ -1343,16 +1342,13 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     Tile<W, NHD> t[MT];
     h4 gc[MT];
     bool dens[MT];
-    BwdFrags<W, NHD> bw;
     {
       bool valid[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) valid[mt] = full || tile * TR + mt * 16 + li < a.M;
       FwdWeights<W, NHD> fwl;
       fwl.load(wbt, lane);
-      bw.load_d2(wbt, lane);
       tile_forward<W, NHD, MT, BF>(fwl, cur, valid, g, t, NoSink{});
-      bw.load_rest(wbt, lane);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         dens[mt] = (REF ? r16(t[mt].po[0]) : t[mt].po[0]) > 0.0f;
@@ -1365,8 +1361,15 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     }
     auto last = [&](int mt, int kt) -> h4 { return NHD == 2 ? t[mt].hd1[kt] : t[mt].hd0[kt]; };
     // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
+    // Each layer's W^T fragments are read from LDS at the start of the layer and pinned
+    // there (sched_barrier): the dW half of the layer, which needs no weights, then covers
+    // the LDS latency that a read placed at its use exposes (1 wave/SIMD).
     h4 dl[MT][NT];
     {
+      h4 wd2[NT];
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) wd2[kt] = bfrag16(N::oBD2 + kt * N::F16);
+      __builtin_amdgcn_sched_barrier(0);
       h8 ga[NP];
 #pragma unroll
       for (int pr = 0; pr < NP; ++pr)
@@ -1378,14 +1381,17 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
           const h8 xl = cat(trc(R0 + 2 + 2 * kt, last(2 * pr, kt)), trc(R0 + 3 + 2 * kt, last(2 * pr + 1, kt)));
           mma32_acc_v<BF>(dD2[kt], ga[pr], xl);
         }
-        const h4 wf = bw.d2[kt];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) dl[mt][kt] = mask_h4<BF>(mma16<BF>(wf, gc[mt], z4), last(mt, kt));
+        for (int mt = 0; mt < MT; ++mt) dl[mt][kt] = mask_h4<BF>(mma16<BF>(wd2[kt], gc[mt], z4), last(mt, kt));
       }
     }
     // ---- dir hidden layer 1 (NHD == 2): dW_D1 (W x W) += dl^T · X_d0 ; dh0 = D1^T dl
     h4 dh0[MT][NT];
     if constexpr (NHD == 2) {
+      h8 wd1[NT * KB];
+#pragma unroll
+      for (int i = 0; i < NT * KB; ++i) wd1[i] = bfrag32(N::oBD1 + i * N::F32);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int pr = 0; pr < NP; ++pr) {
         h8 gb[NT];
@@ -1406,9 +1412,9 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-          const h8 wf = bw.d1[kt * KB + kb];
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) acc[mt] = mma32<BF>(wf, cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
+          for (int mt = 0; mt < MT; ++mt)
+            acc[mt] = mma32<BF>(wd1[kt * KB + kb], cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
         }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) dh0[mt][kt] = mask_h4<BF>(acc[mt], t[mt].hd0[kt]);
@@ -1422,6 +1428,10 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     // ---- dir input layer: dW_D0 (W x 32, k' order) += dh0^T · X_de ; dpos = D0^T dh0
     h4 dpo[MT];
     {
+      h8 wd0[KB];
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) wd0[kb] = bfrag32(N::oBD0 + kb * N::F32);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int pr = 0; pr < NP; ++pr) {
         h4 a0, a1, b0, b1;
@@ -1440,9 +1450,8 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        const h8 wf = bw.d0[kb];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = mma32<BF>(wf, cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mma32<BF>(wd0[kb], cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -1459,6 +1468,10 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     // ---- pos output layer: dW_P1 (16 x W) += dpo^T · X_ph ; dhp = P1^T dpo
     h4 dhp[MT][NT];
     {
+      h4 wp1[NT];
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) wp1[kt] = bfrag16(N::oBP1 + kt * N::F16);
+      __builtin_amdgcn_sched_barrier(0);
       h8 ga[NP];
 #pragma unroll
       for (int pr = 0; pr < NP; ++pr)
@@ -1470,13 +1483,16 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
           const h8 xp = cat(trc(R1 + 2 + 2 * kt, t[2 * pr].hp[kt]), trc(R1 + 3 + 2 * kt, t[2 * pr + 1].hp[kt]));
           mma32_acc_v<BF>(dP1[kt], ga[pr], xp);
         }
-        const h4 wf = bw.p1[kt];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) dhp[mt][kt] = mask_h4<BF>(mma16<BF>(wf, dpo[mt], z4), t[mt].hp[kt]);
+        for (int mt = 0; mt < MT; ++mt) dhp[mt][kt] = mask_h4<BF>(mma16<BF>(wp1[kt], dpo[mt], z4), t[mt].hp[kt]);
       }
     }
     // ---- pos input layer: dW_P0 (W x 32) += dhp^T · X_pe ; d_enc = P0^T dhp
     {
+      h8 wp0[2 * KB];
+#pragma unroll
+      for (int i = 0; i < 2 * KB; ++i) wp0[i] = bfrag32(N::oBP0 + i * N::F32);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int pr = 0; pr < NP; ++pr) {
         h4 a0, a1, b0, b1;
@@ -1497,9 +1513,9 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-          const h8 wf = bw.p0[kt * KB + kb];
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) acc[mt] = mma32<BF>(wf, cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
+          for (int mt = 0; mt < MT; ++mt)
+            acc[mt] = mma32<BF>(wp0[kt * KB + kb], cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
         }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -1515,11 +1531,6 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         }
       }
     }
-    if constexpr (FAST && FULL) {
-#pragma unroll
-      for (int i = 0; i < 4 * MT; i += 4)
-        asm volatile("" ::"v"(keep[i]), "v"(keep[i + 1]), "v"(keep[i + 2]), "v"(keep[i + 3]));
-    }
     // the last dW MFMAs of the tile have written their accumulators before anything
     // (a loop-exit copy) reads them
     agpr_fence();
@@ -1529,9 +1540,17 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     agpr_pin(dP1);
     agpr_pin(dP0);
   };
-  for (int64_t tile = t_begin; tile < t_full_end; ++tile) process(std::integral_constant<bool, true>{}, tile);
+  {
+    const std::integral_constant<bool, true> full_tile;
+    int64_t tile = t_begin;
+    for (; tile + 1 < t_full_end; tile += 2) {
+      process(full_tile, tile, nr0, nr1);
+      process(full_tile, tile + 1, nr1, nr0);
+    }
+    if (tile < t_full_end) process(full_tile, tile, nr0, nr1);
+  }
   for (int64_t tile = t_full_end > t_begin ? t_full_end : t_begin; tile < t_end; ++tile)
-    process(std::integral_constant<bool, false>{}, tile);
+    process(std::integral_constant<bool, false>{}, tile, nr0, nr1);
 
   agpr_fence();
   agpr_pin(dD2);

@@ -816,10 +816,13 @@ def test_ingp_field_unsupported_and_empty(dev):
 def test_ingp_field_bwd_generations_agree(dev, width, nhd, mma):
     """The register-transposed backward (mode 1), the same with LDS transposes (mode 2) and
     the LDS-tile backward (mode 0) on the same inputs (256 rays x 1024 samples plus a
-    ragged 77-row tail): d_enc bit-identical (the dX chain is the same MFMA sequence on the
-    same operands; the transposes are exact), parameter gradients within 1e-5 relative L2
-    (mode 0's dW contraction visits the 32 samples of a tile in a different K order, and
-    the flush is atomic)."""
+    ragged 77-row tail). bf16 (unscaled): d_enc bit-identical (the dX chain is the same
+    MFMA sequence on the same operands; the transposes are exact), parameter gradients
+    within 1e-5 relative L2 (mode 0's dW contraction visits the 32 samples of a tile in a
+    different K order, and the flush is atomic). f16: each wavefront scales its gradients
+    by a power of two set from its own rows, and the row-to-wavefront partition follows
+    each kernel's occupancy, so where two generations differ in occupancy the scales, and
+    with them which tiny gradients flush to f16 zero, differ: within 1e-4 relative L2."""
     from atmonr_amd import _lib
 
     nb, R, n_per_ray = 4, 256, 1024
@@ -857,9 +860,12 @@ def test_ingp_field_bwd_generations_agree(dev, width, nhd, mma):
         out[mode] = (d_enc, g_pos, g_dir)
     rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
     for m in (0, 2):
-        assert torch.equal(out[m][0], out[1][0]), m
+        if mma == "bf16":
+            assert torch.equal(out[m][0], out[1][0]), m
+        else:
+            assert rel(out[m][0], out[1][0]) <= 1e-4, m
         for i in (1, 2):
-            assert rel(out[m][i], out[1][i]) <= 1e-5, (m, i)
+            assert rel(out[m][i], out[1][i]) <= (1e-5 if mma == "bf16" else 1e-4), (m, i)
 
 
 @pytest.mark.gpu

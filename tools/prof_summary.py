@@ -43,7 +43,7 @@ TAGS = {
     "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32>",
     "hash_bwd_rtstride": "hashgrid_bwd_v2_kernel<3, float, 0, 0>",
     "field_fwd": "field::fwd_kernel<64, 2, false, false, true>",
-    "field_bwd": "field::bwd_rt_kernel<64, 2, true, false, false>",
+    "field_bwd": "field::bwd_rt_kernel<64, 2, true, false, false, false, false>",
     "field_bwd_lds": "field::bwd_kernel<64, 2, true, false, false>",
     "composite_fwd": "rb::fwd_kernel<float, 4, 1, 4>",
     "composite_bwd": "rb::bwd_kernel<float, 4, 1, 4>",

@@ -868,6 +868,58 @@ def test_ingp_field_bwd_generations_agree(dev, width, nhd, mma):
             assert rel(out[m][i], out[1][i]) <= (1e-5 if mma == "bf16" else 1e-4), (m, i)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mma", ["f16", "bf16"])
+@pytest.mark.parametrize("width,nhd", [(64, 2), (64, 1), (32, 2), (32, 1)])
+def test_ingp_field_bwd_relaunch_deterministic(dev, width, nhd, mma, mode):
+    """Guard for the field backward's hand-placed hazard wait states (inline-asm MFMAs and
+    ReLU masks): 12 launches on the same inputs give bit-identical dL/denc and parameter
+    gradients equal up to the atomic flush order (2e-5 of the largest: f32 sums of ~16 K
+    contributions in launch-dependent order; measured 1.0e-6). A missing wait
+    state shows as launch-to-launch differences first (r03: the ReLU-mask asm fed MFMA
+    operands without its two wait states, and the W=32 two-hidden-layer dir weight
+    gradients differed from launch to launch by up to 3x their size)."""
+    from atmonr_amd import _lib
+
+    nb, R, n_per_ray = 4, 64, 256
+    M = R * n_per_ray + 29
+    code = _lib.BF16 if mma == "bf16" else _lib.F16
+    g = torch.Generator(device=dev).manual_seed(width + nhd)
+    lib = _lib.load()
+    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
+    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
+    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
+    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
+    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
+    dirs = torch.rand(R + 1, 3, device=dev, generator=g)
+    s = _lib.stream(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", pb, db, code, pp.data_ptr(), pd.data_ptr(),
+              packed.data_ptr(), s)
+    dcol = torch.randn(M, nb, device=dev, generator=g) * 1e-2
+    dsig = torch.randn(M, device=dev, generator=g) * 1e-3
+    ws_bytes = lib.anr_ingp_field_bwd_workspace_bytes(pb, db, code, M)
+    ws = torch.empty(max(1, ws_bytes // 4), device=dev)
+    prev = lib.anr_ingp_field_force_bwd(mode)
+    try:
+        first = None
+        for _ in range(12):
+            d_enc = torch.empty(M, 32, device=dev)
+            g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
+            _lib.call("anr_ingp_field_bwd", pb, db, code, packed.data_ptr(), enc.data_ptr(), 32,
+                      dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(),
+                      ws.data_ptr() if ws_bytes else None, ws_bytes, s)
+            if first is None:
+                first = (d_enc, g_pos, g_dir)
+                continue
+            assert torch.equal(d_enc, first[0])
+            for a, b in ((g_pos, first[1]), (g_dir, first[2])):
+                assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item()
+    finally:
+        lib.anr_ingp_field_force_bwd(prev)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mma", ["f16", "bf16"])
 @pytest.mark.parametrize("n_per_ray,R,extra,width,nhd", [

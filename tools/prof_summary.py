@@ -37,14 +37,14 @@ def source_sha1(tag: str) -> str | None:
     return hashlib.sha1(open(os.path.join(CSRC, f), "rb").read()).hexdigest()
 
 # bench.py kernel tag -> substring of the mangled/demangled kernel name
-TAGS = {
-    "hash_fwd": "hashgrid_fwd_v6_kernel<3, __half, __half>",
-    "hash_fwd_v1": "hashgrid_fwd_kernel<3, 2, __half, __half>",
+TAGS = {  # prefixes: one instantiation of each per bench run (width / dtype follow --variant, --dtype)
+    "hash_fwd": "hashgrid_fwd_v6_kernel<3,",
+    "hash_fwd_v1": "hashgrid_fwd_kernel<3,",
     "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32>",
     "hash_bwd_rtstride": "hashgrid_bwd_v2_kernel<3, float, 0, 0>",
-    "field_fwd": "field::fwd_kernel<64, 2, false, false, true>",
-    "field_bwd": "field::bwd_rt_kernel<64, 2, true, false, false, false, false>",
-    "field_bwd_lds": "field::bwd_kernel<64, 2, true, false, false>",
+    "field_fwd": "field::fwd_kernel<",
+    "field_bwd": "field::bwd_rt_kernel<",
+    "field_bwd_lds": "field::bwd_kernel<",
     "composite_fwd": "rb::fwd_kernel<float, 4, 1, 4>",
     "composite_bwd": "rb::bwd_kernel<float, 4, 1, 4>",
     "sampler": "sample_uniform_bins_kernel",

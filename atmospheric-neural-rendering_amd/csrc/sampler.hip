@@ -31,6 +31,7 @@ struct PrepDev {
   double scale_d;
   double offset[3];
   double lat_min, lat_range, lon_min, lon_range, h;
+  double k_lat, k_lon, k_h;  // 2 / lat_range, 2 / lon_range, 2 / h (host-computed)
   float alt_compress;
 };
 
@@ -67,28 +68,34 @@ __device__ __forceinline__ void preprocess_point(const PrepDev& P, T px, T py, T
     }
     // cartesian_to_horizontal, wgs_84.py:83-97. The sines and cosines of the angles the
     // reference builds with atan2 are formed from the atan2 arguments instead
-    // (sin(atan2(p, q)) = p / hypot, cos = q / hypot; cos(lon) = x / D): same values to
-    // an f64 ulp or two, far below the f32 rounding of the outputs, at a third of the
-    // transcendental work. Only lon and lat themselves need atan2.
+    // (sin(atan2(p, q)) = p / hypot, cos = q / hypot; cos(lon) = x / D), and every f64
+    // division but five is a multiplication by a reciprocal formed once (alt = x / (cos lat
+    // cos lon) = D rl / X; the degree and range scalings multiply by host-computed
+    // constants): each value moves by an f64 ulp or two, 2^-29 of the f32 rounding of the
+    // outputs, at about half of the f64 instructions (this kernel is f64-issue-bound).
+    // Only lon and lat themselves need atan2.
     const double lon = atan2(y, x);
     const double D = sqrt(x * x + y * y);
-    const double t = z / D, k = kA / kB;
+    const double iD = 1.0 / D;
+    const double t = z * iD, k = kA / kB;
     const double ru = sqrt(t * t + k * k);
-    const double su = t / ru, cu = k / ru;
+    const double iru = 1.0 / ru;
+    const double su = t * iru, cu = k * iru;
     const double Y = z + (kE2 * kB) * (su * su * su);
     const double X = D - (kE * kA) * (cu * cu * cu);
     const double lat = atan2(Y, X);
     const double rl = sqrt(X * X + Y * Y);
-    const double sl = Y / rl, cl = X / rl;
+    const double sl = Y / rl;
     const double Nr = kA / sqrt(1.0 - kE * (sl * sl));
-    const double alt = x / (cl * (x / D)) - Nr;
-    double lat_d = lat * 180.0 / kPi;
-    double lon_d = lon * 180.0 / kPi;
+    const double alt = (D * rl) / X - Nr;
+    constexpr double kDeg = 180.0 / kPi;
+    double lat_d = lat * kDeg;
+    double lon_d = lon * kDeg;
     if (P.shift_lon) lon_d = py_mod(lon_d, 360.0) - 180.0;  // harp2.py:379-380
     // harp2.py:381-383
-    const double a = 2.0 * (lat_d - P.lat_min) / P.lat_range - 1.0;
-    const double b = 2.0 * (lon_d - P.lon_min) / P.lon_range - 1.0;
-    const double c = 2.0 * alt / P.h - 1.0;
+    const double a = (lat_d - P.lat_min) * P.k_lat - 1.0;
+    const double b = (lon_d - P.lon_min) * P.k_lon - 1.0;
+    const double c = alt * P.k_h - 1.0;
     // .to(input dtype) then clip(-1, 1), harp2.py:384-385
     cx = static_cast<T>(a);
     cy = static_cast<T>(b);
@@ -261,6 +268,9 @@ static PrepDev make_prep(const anr_prep_params* p) {
   d.lon_min = p->lon_min;
   d.lon_range = p->lon_range;
   d.h = p->ray_origin_height;
+  d.k_lat = 2.0 / p->lat_range;
+  d.k_lon = 2.0 / p->lon_range;
+  d.k_h = 2.0 / p->ray_origin_height;
   d.alt_compress = p->alt_compress;
   return d;
 }

@@ -11,7 +11,15 @@ the same ray pipeline as ``HARP2Dataset`` (harp2.py:26-429):
 * rays from ``get_rays`` -> ``filter_rays`` -> ``normalize_rays`` (wgs_84.py:223-339);
 * radiance from an analytic field: a band-dependent surface albedo pattern plus Gaussian
   cloud blobs at 1-8 km whose image position moves with the view angle (parallax), so
-  the multi-angle views constrain a 3-D density.
+  the multi-angle views constrain a 3-D density (``radiance_model="parallax"``, the
+  benchmark's); or (``radiance_model="volume"``) each ray's radiance RENDERED through a
+  known extinction field: the same blobs as 3-D Gaussian extinction (km^-1,
+  :meth:`extinction_truth`), a band-dependent cloud colour, and the surface pattern as
+  the surface colour, composited with the reference's ``render_with_surface``
+  (graphics_utils.py:6-77, z in km as instant_ngp.py:219) in f64 at ``truth_samples``
+  bin midpoints along the ray's own sampling geometry (samplers.py:8-47, the horizontal
+  preprocessor for the (lat, lon, alt) of every sample). A trained or extracted
+  extinction can then be scored against the truth (:meth:`score_extinction`).
 
 The object exposes the attributes and methods the pipelines and the trainer use from
 ``HARP2Dataset``: ``config``, ``max_i``, ``lat``/``lon``/``alt``, ``scale``, ``offset``,
@@ -70,6 +78,19 @@ class PointPreprocessor:
         return preprocess_points(coords_xyz, self.params())
 
 
+def render_surface_f64(z_km, color, sigma, color_surf):
+    """graphics_utils.py:6-77 ``render_with_surface`` for one colour channel per ray, f64:
+    z (R, n) km, color (R,), sigma (R, n), color_surf (R,) -> radiance (R,)."""
+    mid = (z_km[:, :-1] + z_km[:, 1:]) / 2
+    mid = torch.cat([z_km[:, :1] * 0, mid, z_km[:, -1:]], dim=1)
+    delta = torch.diff(mid, dim=1)
+    alpha = 1 - torch.exp(-sigma * delta)
+    ones = torch.ones_like(alpha[:, :1])
+    weights = alpha * torch.cumprod(torch.cat([ones, 1 - alpha + 1e-10], dim=1), dim=1)[:, :-1]
+    atmo = color * weights.sum(dim=1)
+    return atmo + (1 - alpha).prod(dim=1) * color_surf
+
+
 def make_preprocessor(lat: torch.Tensor, lon: torch.Tensor, scale: float,
                       offset: torch.Tensor, ray_origin_height: float) -> PointPreprocessor:
     """Ranges exactly as harp2.py:358-370 (f32 min/max over the non-NaN lat/lon)."""
@@ -106,7 +127,11 @@ class SyntheticHARP2Dataset:
     def __init__(self, n_views: int = 90, img_size: int = 512, device="cuda",
                  seed: int = 0, spacing_km: float = 2.5, center=(30.0, -60.0),
                  max_abs_view_angle: float = 45.0, ray_origin_height: float = 20000.0,
-                 chunk: int = 1 << 22):
+                 chunk: int = 1 << 22, radiance_model: str = "parallax",
+                 truth_samples: int = 256):
+        if radiance_model not in ("parallax", "volume"):
+            raise ValueError(f"radiance_model {radiance_model!r}: 'parallax' or 'volume'")
+        self.radiance_model = radiance_model
         self.config = {
             "type": "HARP2",
             "max_abs_view_angle": max_abs_view_angle,
@@ -160,6 +185,8 @@ class SyntheticHARP2Dataset:
         del origins, dirs, lens
 
         self._blobs = self._make_blobs(g, center, img_size * spacing_km)
+        self._center = (float(self.lat.reshape(-1).double().mean()),
+                        float(self.lon.reshape(-1).double().mean()))
         rad = self._radiance(self.lat.reshape(-1).double(), self.lon.reshape(-1).double(),
                              angles.to(dev)[None].expand(P, V).reshape(-1),
                              self.irgb_idx.to(dev)[None].expand(P, V).reshape(-1))
@@ -181,6 +208,13 @@ class SyntheticHARP2Dataset:
         self.ray_alt = self.ray_alt.contiguous()
         self._prep = make_preprocessor(self.lat, self.lon, self.scale, self.offset,
                                        ray_origin_height)
+        if radiance_model == "volume":
+            vol = self._volume_radiance(truth_samples)
+            self.ray_rad = vol.float().contiguous()
+            self.max_i = float(self.ray_rad.max())
+            flat = self.int_arr.reshape(-1).clone()
+            flat[self.ray_filter] = self.ray_rad
+            self.int_arr = flat.view(P, V)
 
     # ------------------------------------------------------------------ radiance model
     @staticmethod
@@ -194,14 +228,22 @@ class SyntheticHARP2Dataset:
             blobs.append((dy, dx, h, r, amp))
         return blobs
 
-    def _radiance(self, lat, lon, angle, band):
-        c_lat = float(lat.mean())
-        c_lon = float(lon.mean())
+    def _local_km(self, lat, lon):
+        """(ky, kx): km north / east of the scene centre (flat-earth, as the blobs)."""
+        c_lat, c_lon = self._center
         ky = (lat - c_lat) * 111.32
         kx = (lon - c_lon) * 111.32 * math.cos(math.radians(c_lat))
+        return ky, kx
+
+    def _surface(self, lat, lon, band):
+        ky, kx = self._local_km(lat, lon)
         albedo = torch.tensor([0.30, 0.18, 0.14, 0.12], dtype=torch.float64,
                               device=lat.device)[band]
-        surf = albedo * (1.0 + 0.35 * torch.sin(kx / 37.0) * torch.cos(ky / 53.0))
+        return albedo * (1.0 + 0.35 * torch.sin(kx / 37.0) * torch.cos(ky / 53.0))
+
+    def _radiance(self, lat, lon, angle, band):
+        ky, kx = self._local_km(lat, lon)
+        surf = self._surface(lat, lon, band)
         tan = torch.tan(angle.double() * math.pi / 180)
         cloud = torch.zeros_like(surf)
         trans = torch.ones_like(surf)
@@ -212,6 +254,71 @@ class SyntheticHARP2Dataset:
             cloud = cloud + blob * (0.9 - 0.1 * band.double())
             trans = trans * torch.exp(-2.0 * blob)
         return (surf * trans + cloud) * 100.0
+
+    # ------------------------------------------------------------------ volume truth
+    CLOUD_COLOR = (0.9, 0.8, 0.7, 0.6)  # per IRGB band, x 100 like the surface
+
+    def extinction_truth(self, lat, lon, alt_m):
+        """Ground-truth extinction (km^-1) of ``radiance_model="volume"`` at (lat, lon in
+        degrees, alt in m): the blobs of the parallax model as 3-D Gaussians, peak
+        ``amp`` km^-1 at height h km, horizontal e-folding radius r, vertical 0.5 + 0.1 h
+        km (optical depth ~1 through a blob's core)."""
+        ky, kx = self._local_km(lat, lon)
+        hk = alt_m / 1000.0
+        sig = torch.zeros_like(ky, dtype=torch.float64)
+        for dy, dx, h, r, amp in self._blobs:
+            vz = 0.5 + 0.1 * h
+            sig = sig + amp * torch.exp(-((ky - dy) ** 2 + (kx - dx) ** 2) / (r * r)
+                                        - (hk - h) ** 2 / (vz * vz))
+        return sig
+
+    def _coords_to_horizontal(self, c):
+        """Inverse of the horizontal preprocessor's normalisation (harp2.py:381-383):
+        [-1, 1]^3 -> lat, lon (degrees), alt (m)."""
+        p = self._prep
+        lat = p.lat_min + (c[..., 0] + 1.0) / 2.0 * p.lat_range
+        lon = p.lon_min + (c[..., 1] + 1.0) / 2.0 * p.lon_range
+        alt = (c[..., 2] + 1.0) / 2.0 * p.ray_origin_height
+        return lat, lon, alt
+
+    def _volume_radiance(self, n: int, chunk_rays: int = 1 << 15) -> torch.Tensor:
+        """render_with_surface (graphics_utils.py:6-77) of the truth field along every kept
+        ray, f64: n bin midpoints z in [0, len] (samplers.py:37-45 with t = 0.5), z in km
+        (instant_ngp.py:219), colour = CLOUD_COLOR[band], surface colour = the surface
+        pattern at the ray's pixel."""
+        dev = self.ray_dir.device
+        prep = self._prep.params()
+        band = self.ray_irgb_idx
+        px_lat = self.lat.reshape(-1)[self.ray_filter].double()
+        px_lon = self.lon.reshape(-1)[self.ray_filter].double()
+        surf = self._surface(px_lat, px_lon, band) * 100.0
+        cloud = torch.tensor(self.CLOUD_COLOR, dtype=torch.float64, device=dev)[band] * 100.0
+        t = (torch.arange(n, dtype=torch.float64, device=dev) + 0.5) / n
+        out = torch.empty(band.shape[0], dtype=torch.float64, device=dev)
+        km = float(self.scale) / 1000.0
+        for s in range(0, band.shape[0], chunk_rays):
+            e = min(band.shape[0], s + chunk_rays)
+            z = t[None] * self.ray_len_norm[s:e].double()[:, None]
+            pts = self.ray_origin_norm[s:e].double()[:, None] + \
+                self.ray_dir[s:e].double()[:, None] * z[..., None]
+            c = preprocess_points(pts.float(), prep).double()
+            lat, lon, alt = self._coords_to_horizontal(c)
+            sig = self.extinction_truth(lat, lon, alt)
+            out[s:e] = render_surface_f64(z * km, cloud[s:e], sig, surf[s:e])
+        return out
+
+    def score_extinction(self, sigma: torch.Tensor, lat, lon, alt_m) -> dict:
+        """Extracted extinction vs :meth:`extinction_truth` at the same points (units differ
+        by a constant: the pipelines' density is per km of z, extract divides by
+        dataset.scale, scripts/extract.py:209): Pearson r, the least-squares scale and the
+        relative L2 error after it."""
+        truth = self.extinction_truth(lat.double(), lon.double(), alt_m.double()).reshape(-1)
+        pred = sigma.double().reshape(-1)
+        pc, tc = pred - pred.mean(), truth - truth.mean()
+        r = float((pc * tc).sum() / (pc.norm() * tc.norm()).clamp_min(1e-300))
+        k = float((pred * truth).sum() / (pred * pred).sum().clamp_min(1e-300))
+        rel = float((k * pred - truth).norm() / truth.norm().clamp_min(1e-300))
+        return {"pearson_r": r, "scale": k, "rel_l2_after_scale": rel}
 
     # ------------------------------------------------------------------ HARP2Dataset API
     def get_point_preprocessor(self, point_preprocessor: str) -> PointPreprocessor:

@@ -3,8 +3,9 @@
     python tools/hash_fwd_ab.py [--modes 1,0] [--iters 10] [--log2t 19]
 
 Bench coordinates (synthetic HARP2 scene -> fused sampler, 8192 rays x 1024 samples), f16
-table, f16 output; modes as anr_hashgrid_force_v1 (0 = v6, 1 = v1). Every mode's output is
-compared bit for bit with mode 1's. Prints the HIP-event average per mode. (The r02 log's
+table, f16 output; modes as anr_hashgrid_force_v1 (0 = v6, 1 = v1), or "p" for
+anr_hashgrid_fwd_planar (v8, level-pair planes, converted back to rows for the check).
+Every mode's output is compared bit for bit with mode 1's (or mode 0's). Prints the HIP-event average per mode. (The r02 log's
 mode 7, a level-major-plane experiment, was removed from the library after measuring it.)
 """
 
@@ -31,6 +32,7 @@ def main():
     ap.add_argument("--log2t", type=int, default=19)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--modes", default="1,0")
+    ap.add_argument("--views", type=int, default=8)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -40,7 +42,7 @@ def main():
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
     from atmonr_amd.samplers import sample_and_preprocess
 
-    ds = SyntheticHARP2Dataset(n_views=8, img_size=512, device=dev, seed=0)
+    ds = SyntheticHARP2Dataset(n_views=args.views, img_size=512, device=dev, seed=0)
     batch = next(iter(BatchLoader(ds, B, shuffle=True, seed=0)))
     prep = ds.get_point_preprocessor("horizontal").params(ngp_remap=True, alt_compress=8.0)
     _, _, coords = sample_and_preprocess(batch, N, prep)
@@ -50,26 +52,35 @@ def main():
     lib = _lib.load()
     s = _lib.stream(dev)
     outs = {}
-    for mode in [int(m) for m in args.modes.split(",")]:
+    for mode in [m if m == "p" else int(m) for m in args.modes.split(",")]:
         enc = torch.empty(M, 32, device=dev, dtype=torch.float16)
-        prev = lib.anr_hashgrid_force_v1(mode)
+        planes = torch.empty(8, M, 4, device=dev, dtype=torch.float16)
+        prev = lib.anr_hashgrid_force_v1(0 if mode == "p" else mode)
         timer = _lib.KernelTimer()
         for it in range(args.iters + 2):
             if it == 2:
                 timer.__enter__()
-            _lib.call("anr_hashgrid_fwd", ctypes.byref(desc), x.data_ptr(), 3, M,
-                      table.data_ptr(), _lib.F16, enc.data_ptr(), _lib.F16, 32, s,
-                      tag=f"hash_fwd_m{mode}")
+            if mode == "p":
+                _lib.call("anr_hashgrid_fwd_planar", ctypes.byref(desc), x.data_ptr(), 3, M,
+                          table.data_ptr(), _lib.F16, planes.data_ptr(), _lib.F16, s,
+                          tag="hash_fwd_planar")
+            else:
+                _lib.call("anr_hashgrid_fwd", ctypes.byref(desc), x.data_ptr(), 3, M,
+                          table.data_ptr(), _lib.F16, enc.data_ptr(), _lib.F16, 32, s,
+                          tag=f"hash_fwd_m{mode}")
         timer.__exit__(None, None, None)
         torch.cuda.synchronize()
         lib.anr_hashgrid_force_v1(prev)
         for k, v in timer.summary().items():
             print(f"mode {mode}: {k} avg {v['avg_ms']:.4f} ms ({v['launches']} calls)", flush=True)
+        if mode == "p":
+            enc = planes.permute(1, 0, 2).reshape(M, 32)
         outs[mode] = enc
-    ref = outs.get(1)
+    ref = outs.get(1, outs.get(0))
     if ref is not None:
         for m, o in outs.items():
-            print(f"mode {m} equal to mode 1: {torch.equal(o, ref)}", flush=True)
+            print(f"mode {m} equal to mode {1 if 1 in outs else 0}: {torch.equal(o, ref)}",
+                  flush=True)
 
 
 if __name__ == "__main__":

@@ -14,6 +14,9 @@
 //               independent random addresses of an `n_words` table, `iters` per lane ->
 //               a known count of requested bytes, to calibrate rocprofv3 FETCH_SIZE and
 //               the TCC hit rate for this access shape.
+//   ub_xcc_map  each workgroup records HW_REG_XCC_ID (spinning for (1 + b % 8) x `spin`
+//               clocks first, an imbalanced grid like an XCD-partitioned kernel's) -> the
+//               observed workgroup -> XCD placement.
 //
 // Test/measurement infrastructure, not product: built to tools/ubench/libanr_ubench.so
 // by __graft_entry__.build(); bench.py loads it in its untimed phase. Plain C ABI
@@ -138,7 +141,22 @@ __global__ void __launch_bounds__(256) gather_kernel(const uint32_t* __restrict_
   if (acc == 0x12345678u) sink[gid & 255] = acc;  // keeps the loads; never true here
 }
 
+__global__ void __launch_bounds__(256) xcc_map_kernel(uint32_t* __restrict__ out, int spin) {
+  uint32_t xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const long long t0 = clock64();
+  const long long until = static_cast<long long>(spin) * (1 + (blockIdx.x & 7));
+  while (clock64() - t0 < until) __builtin_amdgcn_s_sleep(1);
+  if (threadIdx.x == 0) out[blockIdx.x] = xcc & 0xFu;
+}
+
 extern "C" {
+
+int ub_xcc_map(void* out, int blocks, int spin, void* stream) {
+  if (blocks <= 0 || spin < 0) return 1;
+  xcc_map_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((uint32_t*)out, spin);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 int ub_copy(const void* src, void* dst, int64_t n_float4, int blocks, void* stream) {
   if (n_float4 <= 0 || blocks <= 0) return 1;

@@ -1140,36 +1140,6 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v6_kernel(
       os_bytes);
 }
 
-// ---------------------------------------------------------------------------------------
-// Forward v8 (F = 2, L <= 16, level-pair planes): XCD-affine level partition. On the bench
-// geometry nearly every corner gather of a cell the walk enters misses L2 when all 16
-// levels share it (3.9 TCC misses per sample, 211 B of gather fetch), while one level
-// pair alone (at most 2 x 2 MiB of f16 table) stays L2-resident (0.2-0.5 misses per
-// sample; profiles/r03_hash_levels.md). Workgroup b serves level pair p = b % 8 -- the
-// dispatcher deals workgroups to the 8 XCDs round-robin, so each XCD's L2 holds one
-// pair's tables (results do not depend on that mapping, only the speed) -- for 128
-// chunks of K samples: lane = (chunk, level of the pair). Output: one plane per pair,
-// enc_planes[p][m][2 levels][2 features], so every XCD writes whole lines. Same walk,
-// corner order and fma chain as v6: bit-identical values.
-template <int D, typename TT, typename TO>
-__global__ void __launch_bounds__(256) hashgrid_fwd_v8_kernel(
-    GridLevels G, int n_levels, const float* __restrict__ x, uint32_t x_bytes, uint32_t xs4,
-    int64_t M, int K, const TT* __restrict__ table, uint32_t table_bytes,
-    TO* __restrict__ out, uint32_t out_bytes) {
-  const int pair = static_cast<int>(blockIdx.x & 7u);
-  const int level = 2 * pair + static_cast<int>(threadIdx.x & 1u);
-  const int64_t chunk = static_cast<int64_t>(blockIdx.x >> 3) * (blockDim.x >> 1) + (threadIdx.x >> 1);
-  const int64_t m0 = chunk * K;
-  if (level >= n_levels || m0 >= M) return;
-  constexpr uint32_t row = 4u * sizeof(TO);  // 2 levels x 2 features
-  fwd_walk_v6<D, TT, TO>(
-      G, level, m0, K, wave_rsrc(x, x_bytes), xs4, wave_rsrc(table, table_bytes),
-      wave_rsrc(out, out_bytes),
-      static_cast<uint32_t>(pair) * static_cast<uint32_t>(M) * row +
-          static_cast<uint32_t>(m0) * row + static_cast<uint32_t>(level & 1) * 2u * sizeof(TO),
-      row);
-}
-
 // XS / DS: compile-time coordinate and dL/dy row strides (0 = the run-time x_stride /
 // dout_stride). With both known (the fused field's (M,3) coordinates and (M,32) dL/denc)
 // every prefetch address is a per-batch scalar base plus immediate offsets: the walk
@@ -1620,56 +1590,6 @@ extern "C" int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x,
   ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_fwd: descriptor not initialised");
   ANR_HG_DISPATCH(launch_fwd, G, d, x, x_stride, M, table, table_dtype, out, out_dtype,
                   out_stride, as_stream(stream));
-}
-
-extern "C" int anr_hashgrid_fwd_planar(const anr_hashgrid_desc* d, const float* x,
-                                       int64_t x_stride, int64_t M, const void* table,
-                                       int32_t table_dtype, void* out, int32_t out_dtype,
-                                       anr_stream_t stream) {
-  using namespace anr;
-  ANR_CHECK_ARG(d && x && table && out, "anr_hashgrid_fwd_planar: null argument");
-  ANR_CHECK_ARG(d->n_features == 2 && (d->n_dims == 2 || d->n_dims == 3) &&
-                    d->n_levels >= 1 && d->n_levels <= 16,
-                "anr_hashgrid_fwd_planar: needs 2 features per level, 2-3 dims, <= 16 levels");
-  ANR_CHECK_ARG(M >= 0 && x_stride >= d->n_dims, "anr_hashgrid_fwd_planar: bad shape/stride");
-  ANR_CHECK_ARG((table_dtype == ANR_F16 || table_dtype == ANR_F32) &&
-                    (out_dtype == ANR_F16 || out_dtype == ANR_F32),
-                "anr_hashgrid_fwd_planar: bad dtype");
-  if (M == 0) return ANR_OK;
-  GridLevels G;
-  ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_fwd_planar: descriptor not initialised");
-  const int64_t esz_t = table_dtype == ANR_F16 ? 2 : 4, esz_o = out_dtype == ANR_F16 ? 2 : 4;
-  const int64_t K = pick_chunk(M);
-  const int64_t x_bytes = ((M - 1) * x_stride + d->n_dims) * 4;
-  const int64_t t_bytes =
-      static_cast<int64_t>(G.offset[d->n_levels - 1] + G.size[d->n_levels - 1]) * 2 * esz_t;
-  const int64_t o_bytes = 8 * M * 4 * esz_o;  // 8 pair planes (unused ones never written)
-  const int64_t lim = int64_t(1) << 31;
-  ANR_CHECK_ARG(x_bytes < lim && t_bytes < lim && o_bytes < lim && (M + K) * x_stride * 4 < lim,
-                "anr_hashgrid_fwd_planar: buffers past 2 GiB");
-  const int64_t groups = ceil_div(ceil_div(M, K), 128);
-  const dim3 grid(static_cast<unsigned>(groups * 8)), block(256);
-  const hipStream_t s = as_stream(stream);
-#define ANR_HG_FWD8(DD, TT, TO)                                                               \
-  hipLaunchKernelGGL((hashgrid_fwd_v8_kernel<DD, TT, TO>), grid, block, 0, s, G, d->n_levels, \
-                     x, static_cast<uint32_t>(x_bytes), static_cast<uint32_t>(x_stride * 4), M, \
-                     static_cast<int>(K), static_cast<const TT*>(table),                       \
-                     static_cast<uint32_t>(t_bytes), static_cast<TO*>(out),                    \
-                     static_cast<uint32_t>(o_bytes))
-#define ANR_HG_FWD8_T(DD)                                                              \
-  if (table_dtype == ANR_F16 && out_dtype == ANR_F16) ANR_HG_FWD8(DD, __half, __half); \
-  else if (table_dtype == ANR_F16) ANR_HG_FWD8(DD, __half, float);                     \
-  else if (out_dtype == ANR_F16) ANR_HG_FWD8(DD, float, __half);                       \
-  else ANR_HG_FWD8(DD, float, float)
-  if (d->n_dims == 3) {
-    ANR_HG_FWD8_T(3);
-  } else {
-    ANR_HG_FWD8_T(2);
-  }
-#undef ANR_HG_FWD8_T
-#undef ANR_HG_FWD8
-  ANR_CHECK_LAUNCH("anr_hashgrid_fwd_planar");
-  return ANR_OK;
 }
 
 extern "C" int anr_hashgrid_bwd(const anr_hashgrid_desc* d, const float* x,

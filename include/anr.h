@@ -144,16 +144,6 @@ int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x, int64_t x_strid
                      int64_t M, const void* table, int32_t table_dtype, void* out,
                      int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
 
-/* Forward, level-pair planes (XCD-affine; F = 2, n_levels <= 16): same values as
- * anr_hashgrid_fwd, written as out[p][m][j][f] = feature f of level 2p + j for sample m
- * (8 planes of M x 4 values, out_dtype; planes past ceil(n_levels / 2) and the second
- * level of a final odd pair are not written). Workgroups of pair p are dealt to one
- * XCD so its L2 holds only that pair's tables. Replaces the same tcnn call site as
- * anr_hashgrid_fwd (src/atmonr/pipelines/instant_ngp.py:60-63,163). */
-int anr_hashgrid_fwd_planar(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
-                            int64_t M, const void* table, int32_t table_dtype, void* out,
-                            int32_t out_dtype, anr_stream_t stream);
-
 /* Kernel generation (test / A-B hook; process-wide; returns the previous mode; also
  * ANR_HASHGRID_MODE): 0 = default (forward v6 branch-free walker -- v1 above 16 levels or
  * past 32-bit buffer offsets -- backward v2 four-lanes-per-level), 1 = v1 both,

@@ -4,7 +4,8 @@
 
 Bench coordinates (synthetic HARP2 scene -> fused sampler, 8192 rays x 1024 samples), f16
 table, f16 output; modes as anr_hashgrid_force_v1 (0 = v6, 1 = v1), or "p" for
-anr_hashgrid_fwd_planar (v8, level-pair planes, converted back to rows for the check).
+anr_hashgrid_fwd_planar (v8, level-pair planes, converted back to rows for the check;
+removed from the library after profiles/r03_hash_levels.md §3).
 Every mode's output is compared bit for bit with mode 1's (or mode 0's). Prints the HIP-event average per mode. (The r02 log's
 mode 7, a level-major-plane experiment, was removed from the library after measuring it.)
 """

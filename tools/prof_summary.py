@@ -79,7 +79,10 @@ def main(src: str, tag: str, key_suffix: str = "baseline:8192x1024"):
              "bench.py (config-3 train step, 8192 rays x 1024 samples), "
              "`rocprofv3 --kernel-trace --stats` plus separate `--pmc FETCH_SIZE` and "
              "`--pmc WRITE_SIZE` passes (tools/prof.sh). Traffic = (2*FETCH_SIZE + "
-             "WRITE_SIZE) KiB per launch (gfx950 FETCH_SIZE half-count correction).", "",
+             "WRITE_SIZE) KiB per launch (gfx950 FETCH_SIZE half-count correction; the "
+             "hash-grid forward's 4-B gathers are counted in full, so its calibrated "
+             "traffic in profiles/pmc_traffic.json is FETCH + 6 B/sample + WRITE: "
+             "profiles/r03_hash_levels.md).", "",
              "Steady avg = mean duration over the second half of each kernel's launches in "
              "the kernel trace (the bench network is alive from step ~7; the first steps' "
              "backward skips its zero-gradient atomics).", "",
@@ -113,6 +116,14 @@ def main(src: str, tag: str, key_suffix: str = "baseline:8192x1024"):
         if f is not None and w is not None:
             ent = {"bytes": round((2 * f + w) * 1024), "fetch_kib": round(f, 1),
                    "write_kib": round(w, 1), "source": tag}
+            if t.startswith("hash_fwd"):
+                # 4-B corner gathers: FETCH_SIZE counts the 64 B of each miss in full
+                # (tools/ubench gather_calib, profiles/r03_hash_levels.md); only the
+                # 12-B/sample coordinate stream is half-counted
+                B, N = (int(v) for v in key_suffix.rsplit(":", 1)[1].split("x"))
+                ent["bytes"] = round(f * 1024 + 6 * B * N + w * 1024)
+                ent["calibration"] = ("FETCH_SIZE not doubled for the 4-B gathers; "
+                                      "+6 B/sample for the half-counted coordinates")
             if a:  # TCC_EA0_ATOMIC_sum: memory-side atomic requests (64-B segments)
                 ent["atomic_requests"] = round(a)
             ent["kernel_source_sha1"] = source_sha1(t)

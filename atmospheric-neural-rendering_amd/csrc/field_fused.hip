@@ -578,8 +578,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* p, int64_
                                            0x00020000);
 }
 
+// Four waves per SIMD: at the compiler's free choice the W = 64 forward took 136 VGPRs
+// (3 waves); capped at 128 it fits in 126 without spills, and the fourth wave hides more
+// of the per-tile prefetch latency (field fwd 0.204 -> 0.201 ms, step -0.02 ms;
+// profiles/r03_field_fwd_occ.log). The grid is sized from the same occupancy query.
 template <int W, int NHD, bool ROWS, bool BF, bool UT>
-__global__ void __launch_bounds__(256) fwd_kernel(Args a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) fwd_kernel(Args a) {
   static_assert(!(UT && ROWS), "the uniform-tile form needs dense rows");
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   // wave index through readfirstlane: the tile loop then runs on scalar registers

@@ -2,6 +2,7 @@
 # r03: field forward at 4 waves per SIMD (amdgpu_waves_per_eu(4): 136 -> 126 VGPRs,
 # exp_libs/libanr_ffw4.so) against the product library (3 waves): field GPU tests on the
 # variant, then alternating bench.py runs (ms/step, profiling-pass field_fwd avg).
+# (Record: the variant is now the product form, field_fused.hip fwd_kernel.)
 set -o pipefail
 OUT=${1:-gpurun_out/ffw}; mkdir -p "$OUT"
 LIB=$PWD/exp_libs/libanr_ffw4.so

@@ -1,6 +1,7 @@
 #!/bin/bash
 # r03: hash backward occupancy sweep (prefetch batch HASH_BS x waves-per-SIMD cap) with and
 # without x-carry (modes 0 / 8): exp_libs/libanr_<variant>.so against the product library.
+# (Record: the exp_libs variants were built from hashgrid.hip with -DHASH_BS / amdgpu_waves_per_eu on the x-carry kernel, removed after the run.)
 set -o pipefail
 OUT=${1:-gpurun_out/occ}; mkdir -p "$OUT"
 for r in 1 2; do

@@ -1,6 +1,7 @@
 #!/bin/bash
 # r03: hash forward (v6) coordinate-prefetch depth HASH_FBS x occupancy sweep:
 # exp_libs/libanr_<variant>.so against the product library (FBS 4, 88 VGPRs, 5 waves/SIMD).
+# (Record: the exp_libs variants were built from hashgrid.hip with -DHASH_FBS / amdgpu_waves_per_eu(6); none kept.)
 set -o pipefail
 for r in 1 2; do
   for v in cand fbs1 fbs2 fbs3w6; do

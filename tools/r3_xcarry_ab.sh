@@ -1,7 +1,7 @@
 #!/bin/bash
 # r03: hash backward x-carry (mode 8) against the v2 default (mode 0): hash-grid parity
-# (Record of a removed experiment: mode 8 left the library after this run; profiles/r03_hash_bwd_xcarry_ab.log.)
 # tests, HIP-event A/B at bench size, memory-side atomic requests per launch (PMC).
+# (Record of a removed experiment: mode 8 left the library after this run; profiles/r03_hash_bwd_xcarry_ab.log.)
 set -o pipefail
 OUT=${1:-gpurun_out/xc}; mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -110,6 +110,7 @@ class AdamTensor(Structure):
 
 
 ADAM_MAX_TENSORS = 16
+ADAM_DEV_MAX_TENSORS = 64
 
 
 class GatherCol(Structure):
@@ -291,6 +292,9 @@ _SIGNATURES = {
     "anr_adam_step_multi": (
         c_int32, [_P, c_int32, c_float, c_float, c_float, c_int32, c_int32, _P],
     ),
+    "anr_adam_step_multi_dev": (
+        c_int32, [_P, c_int32, c_float, c_float, c_float, c_int32, c_int32, _P, _P, _P, _P],
+    ),
 }
 
 _lib = None
@@ -300,11 +304,14 @@ _timer = None  # optional KernelTimer: HIP events around every entry-point call
 class KernelTimer:
     """Records a (start, end) torch.cuda.Event pair on the current stream around each
     libanr_hip call, keyed by entry-point name or tag (bench.py's per-kernel timing).
-    ``only``: time just these names/tags (the other calls run without events)."""
+    ``only``: time just these names/tags (the other calls run without events).
+    ``external``: events that a hipGraph capture records as event-record nodes (each
+    replay re-records them), for timing a kernel inside a captured step."""
 
-    def __init__(self, only: set[str] | None = None):
+    def __init__(self, only: set[str] | None = None, external: bool = False):
         self.events: dict[str, list] = {}
         self.only = set(only) if only is not None else None
+        self.external = external
 
     def __enter__(self):
         global _timer
@@ -354,8 +361,9 @@ def call(name: str, *args, tag: str | None = None) -> int:
     for the KernelTimer (defaults to the entry-point name)."""
     lib = load()
     if _timer is not None and (_timer.only is None or (tag or name) in _timer.only):
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
+        kw = {"external": True} if _timer.external else {}
+        a = torch.cuda.Event(enable_timing=True, **kw)
+        b = torch.cuda.Event(enable_timing=True, **kw)
         a.record()
         rc = getattr(lib, name)(*args)
         b.record()

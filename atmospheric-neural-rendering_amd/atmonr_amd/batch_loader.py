@@ -66,6 +66,15 @@ class BatchLoader:
             out.append((base + r * q, base + (r + 1) * q))
         return out
 
+    def index_batches(self) -> Iterator[torch.Tensor]:
+        """The ray indices of this rank's batches of the next epoch (device int64 slices of
+        the permutation): what __iter__ gathers, for callers that gather themselves (a
+        captured step reads its rows from a static index buffer, atmonr_amd.graph)."""
+        perm = self._perm()
+        self.epoch += 1
+        for s, e in self.slices():
+            yield perm[s:e]
+
     def __iter__(self) -> Iterator[dict[str, torch.Tensor]]:
         perm = self._perm()
         self.epoch += 1

@@ -4,6 +4,14 @@ Drop-in for torch.optim.AdamW (instant_ngp.py:120-126; ``decoupled=True``) and
 torch.optim.Adam (nerf.py:70; ``decoupled=False``): same param-group semantics, same
 state keys (``step``, ``exp_avg``, ``exp_avg_sq``) so optimizer state dicts interchange
 with torch's.
+
+``capturable=True`` (as torch.optim.AdamW's flag of that name): the step count and the
+learning rates live in device memory (anr_adam_step_multi_dev), so ``step()`` launches
+the same kernels with the same arguments every time and can be captured in a hipGraph
+(atmonr_amd.graph). The host copy of ``state["step"]`` is refreshed from the device by
+``state_dict()``; learning-rate changes (schedulers write ``group["lr"]``) reach the
+device in ``sync_hyper()``, which ``step()`` calls outside a capture and a graph replay
+calls before launching.
 """
 
 from __future__ import annotations
@@ -18,7 +26,8 @@ from ._lib import call, ptr
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=None,
-                 decoupled: bool = True, zero_grad_in_step: bool = False, **unused):
+                 decoupled: bool = True, zero_grad_in_step: bool = False,
+                 capturable: bool = False, **unused):
         if weight_decay is None:  # torch.optim.AdamW's default 1e-2, Adam's 0
             weight_decay = 1e-2 if decoupled else 0.0
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay)
@@ -29,6 +38,109 @@ class FusedAdam(torch.optim.Optimizer):
         self.zero_grad_in_step = zero_grad_in_step
         self.zeroed_buckets: list = []  # FlatGradBucket.fuse_zero_into
         self.multi_tensor = True  # one anr_adam_step_multi launch per step and device
+        self.capturable = capturable
+        self._devstate: dict = {}  # capturable: (device, b1, b2, eps) -> device step / lr
+
+    # ------------------------------------------------------------------ capturable mode
+    def _entries(self):
+        """(key, param, group) of every parameter with a gradient, launch order."""
+        out = []
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            key_hp = (float(b1), float(b2), float(group["eps"]))
+            for p in group["params"]:
+                if p.grad is not None:
+                    out.append(((p.device,) + key_hp, p, group))
+        return out
+
+    def _init_state(self, p):
+        if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+            raise _lib.ANRError("FusedAdam needs float32 params and grads")
+        st = self.state[p]
+        if not st:
+            st["step"] = torch.tensor(0.0)
+            st["exp_avg"] = torch.zeros_like(p)
+            st["exp_avg_sq"] = torch.zeros_like(p)
+        if st["step"].device.type != "cpu":
+            st["step"] = st["step"].cpu()
+        if not p.grad.is_contiguous():
+            p.grad = p.grad.contiguous()
+        return st
+
+    def sync_hyper(self) -> None:
+        """Write changed learning rates to the device (capturable mode; outside a capture)."""
+        for ds in self._devstate.values():
+            lrs = [float(g["lr"]) for g in ds["groups"]]
+            if lrs != ds["lr_host"]:
+                ds["lr"].copy_(torch.tensor(lrs, dtype=torch.float32))
+                ds["lr_host"] = lrs
+
+    def _prepare(self):
+        """Device step / lr buffers per launch key, built eagerly (never inside a capture:
+        their initial values must not be part of the graph)."""
+        batches: dict = {}
+        for key, p, group in self._entries():
+            batches.setdefault(key, []).append((p, group))
+        if set(batches) != set(self._devstate):
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.ANRError("FusedAdam(capturable=True): run one step eagerly before "
+                                    "capturing it (the device step/lr state is built then)")
+            self._devstate = {}
+            for key, items in batches.items():
+                if len(items) > _lib.ADAM_DEV_MAX_TENSORS:
+                    raise _lib.ANRError(f"capturable FusedAdam: at most "
+                                        f"{_lib.ADAM_DEV_MAX_TENSORS} tensors per launch")
+                dev = key[0]
+                sts = [self._init_state(p) for p, _ in items]
+                step0 = int(sts[0]["step"].item())
+                if any(int(st["step"].item()) != step0 for st in sts):
+                    raise _lib.ANRError("capturable FusedAdam: parameters at different steps")
+                self._devstate[key] = {
+                    "params": [p for p, _ in items], "groups": [g for _, g in items],
+                    "step": torch.tensor([step0], dtype=torch.int64, device=dev),
+                    "lr": torch.tensor([float(g["lr"]) for _, g in items], device=dev),
+                    "lr_host": [float(g["lr"]) for _, g in items],
+                    "scratch": torch.zeros(3 * _lib.ADAM_DEV_MAX_TENSORS, device=dev)}
+        return batches
+
+    def _step_capturable(self):
+        batches = self._prepare()
+        if not torch.cuda.is_current_stream_capturing():
+            self.sync_hyper()
+        for key, items in batches.items():
+            dev, b1, b2, eps = key
+            ds = self._devstate[key]
+            ts = []
+            for p, group in items:
+                st = self._init_state(p)
+                sh = getattr(p, "_anr_shadow", None)
+                if sh is not None and (sh.dtype != torch.float16 or sh.shape != p.shape):
+                    sh = None
+                ts.append(_lib.AdamTensor(ptr(p), ptr(p.grad), ptr(st["exp_avg"]),
+                                          ptr(st["exp_avg_sq"]), ptr(sh), p.numel(),
+                                          float(group["lr"]), float(group["weight_decay"]), 0))
+                if sh is not None:
+                    p._anr_shadow_ver = p._version
+            arr = (_lib.AdamTensor * len(ts))(*ts)
+            call("anr_adam_step_multi_dev", ctypes.addressof(arr), len(ts), b1, b2, eps,
+                 int(self.decoupled), int(self.zero_grad_in_step), ptr(ds["step"]),
+                 ptr(ds["lr"]), ptr(ds["scratch"]), _lib.stream(dev), tag="adam")
+
+    def device_step(self) -> int:
+        """The step count held on the device (capturable mode; synchronises)."""
+        return max((int(ds["step"].item()) for ds in self._devstate.values()), default=0)
+
+    def state_dict(self):
+        if self.capturable:
+            for ds in self._devstate.values():
+                n = float(ds["step"].item())
+                for p in ds["params"]:
+                    self.state[p]["step"] = torch.tensor(n)
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._devstate = {}  # rebuilt from the loaded host steps at the next step()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -38,6 +150,12 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self.capturable:
+            self._step_capturable()
+            if self.zero_grad_in_step:
+                for b in self.zeroed_buckets:
+                    b.mark_zero()
+            return loss
         # (device, beta1, beta2, eps) -> [anr_adam_tensor]: groups with their own betas /
         # eps get their own launch, as torch.optim.Adam(W) steps each group with its own
         batches: dict = {}

@@ -193,6 +193,16 @@ class Trainer:
                 self.writer.add_scalar("Loss", v, start + i)
         running.extend(vals)
         del running[: max(0, len(running) - int(self.config["print_frequency"]) - 1)]
+        zr = getattr(self.pipeline, "zero_rays_total", 0)  # reference numerics only
+        if zr and zr != getattr(self, "_zero_rays_seen", 0):
+            self._zero_rays_seen = zr
+            import warnings
+
+            warnings.warn(f"numerics='reference': {zr} rays so far had an f16 alpha of exactly "
+                          "1 and trained with zero gradients (torch's zero-input cumprod "
+                          "backward is not reproduced)", RuntimeWarning)
+            if self.writer is not None:
+                self.writer.add_scalar("ZeroGradRays", zr, self.iter_count)
 
     def _end_epoch(self, output_path: Path | None) -> None:
         self._gather_progress()

@@ -109,6 +109,86 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamTensors a, float b1
   }
 }
 
+// Device-step form (hipGraph capture): the step count and every tensor's lr live in
+// caller-owned device memory, so one captured launch pair serves every replay. The tick
+// kernel advances the step and forms each tensor's scalars in double, as adam_scalars
+// does on the host; the update kernel reads them (block-uniform scalar loads) and runs
+// adam_multi_kernel's per-element arithmetic.
+struct AdamWd {
+  float v[ANR_ADAM_DEV_MAX_TENSORS];
+};
+
+__global__ void adam_tick_kernel(int64_t* __restrict__ d_step, const float* __restrict__ d_lr,
+                                 AdamWd wd, float beta1, float beta2, int n,
+                                 float* __restrict__ scal) {
+  const int t = threadIdx.x;
+  const int64_t step = *d_step + 1;
+  __syncthreads();  // every thread has read the old count before thread 0 writes
+  if (t == 0) *d_step = step;
+  if (t >= n) return;
+  const double lr = static_cast<double>(d_lr[t]);
+  const double bc1 = 1.0 - pow(static_cast<double>(beta1), static_cast<double>(step));
+  const double bc2 = 1.0 - pow(static_cast<double>(beta2), static_cast<double>(step));
+  scal[3 * t + 0] = static_cast<float>(lr / bc1);
+  scal[3 * t + 1] = static_cast<float>(sqrt(bc2));
+  scal[3 * t + 2] = static_cast<float>(1.0 - lr * static_cast<double>(wd.v[t]));
+}
+
+struct AdamTensorsDev {
+  float* p[ANR_ADAM_MAX_TENSORS];
+  float* g[ANR_ADAM_MAX_TENSORS];
+  float* m[ANR_ADAM_MAX_TENSORS];
+  float* v[ANR_ADAM_MAX_TENSORS];
+  __half* p16[ANR_ADAM_MAX_TENSORS];
+  int64_t n[ANR_ADAM_MAX_TENSORS];
+  float wd[ANR_ADAM_MAX_TENSORS];
+  int idx[ANR_ADAM_MAX_TENSORS];  // the tensor's index in the caller's array (its scalars)
+  int first[ANR_ADAM_MAX_TENSORS + 1];
+  int count;
+};
+
+__global__ void __launch_bounds__(256) adam_multi_dev_kernel(AdamTensorsDev a,
+                                                             const float* __restrict__ scal,
+                                                             float b1, float b2, float eps,
+                                                             int decoupled, int zero_grad) {
+  int t = 0;  // block-uniform
+  while (t + 1 < a.count && static_cast<int>(blockIdx.x) >= a.first[t + 1]) ++t;
+  float* __restrict__ p = a.p[t];
+  float* __restrict__ g = a.g[t];
+  float* __restrict__ m = a.m[t];
+  float* __restrict__ v = a.v[t];
+  __half* __restrict__ p16 = a.p16[t];
+  const int64_t n = a.n[t];
+  const float wd = a.wd[t];
+  const float step_size = scal[3 * a.idx[t] + 0], bc2_sqrt = scal[3 * a.idx[t] + 1],
+              decay = scal[3 * a.idx[t] + 2];
+  const float w1 = 1.0f - b1;
+  const int64_t base = static_cast<int64_t>(static_cast<int>(blockIdx.x) - a.first[t]) * 1024;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    if (i >= n) break;
+    float pi = p[i];
+    float gi = g[i];
+    if (wd != 0.0f) {
+      if (decoupled)
+        pi = pi * decay;
+      else
+        gi = gi + wd * pi;
+    }
+    float mi = m[i];
+    mi = w1 < 0.5f ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.0f - w1);
+    float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi + (-step_size) * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+    if (p16) p16[i] = __float2half_rn(pi);
+    if (zero_grad) g[i] = 0.0f;
+  }
+}
+
 // torch's bias corrections and decoupled decay factor, in Python double
 static void adam_scalars(float lr, float beta1, float beta2, float weight_decay, int64_t step,
                          float* step_size, float* bc2_sqrt, float* decay) {
@@ -187,5 +267,57 @@ extern "C" int anr_adam_step(float* params, float* grad, float* exp_avg, float* 
                      static_cast<__half*>(params_f16), n, lr, beta1, beta2, eps, weight_decay,
                      decay, decoupled, step_size, bc2_sqrt, zero_grad);
   ANR_CHECK_LAUNCH("anr_adam_step");
+  return ANR_OK;
+}
+
+extern "C" int anr_adam_step_multi_dev(const anr_adam_tensor* tensors, int32_t n_tensors,
+                                       float beta1, float beta2, float eps, int32_t decoupled,
+                                       int32_t zero_grad, int64_t* d_step, const float* d_lr,
+                                       float* d_scratch, anr_stream_t stream) {
+  using namespace anr;
+  ANR_CHECK_ARG(n_tensors >= 0 && n_tensors <= ANR_ADAM_DEV_MAX_TENSORS &&
+                    (n_tensors == 0 || tensors),
+                "anr_adam_step_multi_dev: 0..%d tensors", ANR_ADAM_DEV_MAX_TENSORS);
+  ANR_CHECK_ARG(d_step && d_lr && d_scratch, "anr_adam_step_multi_dev: null device state");
+  for (int32_t i = 0; i < n_tensors; ++i) {
+    const anr_adam_tensor& d = tensors[i];
+    ANR_CHECK_ARG(d.n >= 0, "anr_adam_step_multi_dev: tensor %d: bad size", i);
+    ANR_CHECK_ARG(d.n == 0 || (d.params && d.grad && d.exp_avg && d.exp_avg_sq),
+                  "anr_adam_step_multi_dev: tensor %d: null pointer", i);
+  }
+  AdamWd wd;
+  memset(&wd, 0, sizeof(wd));
+  for (int32_t i = 0; i < n_tensors; ++i) wd.v[i] = tensors[i].weight_decay;
+  hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(ANR_ADAM_DEV_MAX_TENSORS), 0,
+                     as_stream(stream), d_step, d_lr, wd, beta1, beta2, n_tensors, d_scratch);
+  ANR_CHECK_LAUNCH("anr_adam_step_multi_dev (tick)");
+  int32_t t = 0;
+  while (t < n_tensors) {
+    AdamTensorsDev a;
+    memset(&a, 0, sizeof(a));
+    int64_t blocks = 0;
+    for (; t < n_tensors && a.count < ANR_ADAM_MAX_TENSORS; ++t) {
+      const anr_adam_tensor& d = tensors[t];
+      if (d.n == 0) continue;
+      const int c = a.count++;
+      a.p[c] = d.params;
+      a.g[c] = d.grad;
+      a.m[c] = d.exp_avg;
+      a.v[c] = d.exp_avg_sq;
+      a.p16[c] = static_cast<__half*>(d.params_f16);
+      a.n[c] = d.n;
+      a.wd[c] = d.weight_decay;
+      a.idx[c] = t;
+      a.first[c] = static_cast<int>(blocks);
+      blocks += ceil_div(d.n, 1024);
+      ANR_CHECK_ARG(blocks < (int64_t(1) << 31), "anr_adam_step_multi_dev: too many elements");
+    }
+    if (a.count == 0) continue;
+    a.first[a.count] = static_cast<int>(blocks);
+    hipLaunchKernelGGL(adam_multi_dev_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                       as_stream(stream), a, d_scratch, beta1, beta2, eps, decoupled,
+                       zero_grad);
+    ANR_CHECK_LAUNCH("anr_adam_step_multi_dev");
+  }
   return ANR_OK;
 }

@@ -254,6 +254,277 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
         dist.destroy_process_group()
 
 
+def run_extract(args, ds, dev, rank, world, t_scene):
+    """Extract throughput (scripts/extract.py:180-211 ->
+    InstantNGPPipeline.extract, instant_ngp.py:208-247): the reference loop over an
+    L1C-style grid of the scene's 512x512 columns x 81 altitudes (alt_step 250 m, 0 to
+    20 km: harp2_extract.py's grid), batches of 32,768 columns x 81 = 2,654,208 points, unshuffled.
+    One step = one batch: (xyz - offset) / scale in f64, the f64 preprocessor kernel, the
+    hash-grid forward and the field's density, sigma[idx] = . / scale. Forward-only,
+    random-init weights. Ranks take disjoint batches (no collective); `value` is points/s
+    over all ranks."""
+    from atmonr_amd import _lib
+    from atmonr_amd.batch_loader import BatchLoader
+    from atmonr_amd.extract import GridExtractDataset
+    from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
+
+    peaks = measured_peaks(dev, args.spec_peaks)
+    cfg = ingp_config(args.variant, args.samples)
+    pipe = InstantNGPPipeline(cfg, ds, dtype=torch.float16, fused=True, seed=1337)
+    pipe.send_tensors_to(dev)
+    pipe.eval()
+    grid = GridExtractDataset(ds, alt_step=250.0)
+    A = int(grid.sample_alt.shape[0])
+    cols = args.extract_batch
+    P = cols * A
+    loader = BatchLoader(grid, batch_size=P, shuffle=False, rank=rank, world_size=world)
+    sigma = torch.zeros((len(grid), 1), device=dev)
+    offset = torch.as_tensor(ds.offset, dtype=torch.float64, device=dev)
+    batches = [b for b in loader if b["idx"].shape[0] == P]  # full batches only
+    k = [0]
+
+    @torch.no_grad()
+    def step():
+        b = batches[k[0] % len(batches)]
+        k[0] += 1
+        pts = (b["xyz"] - offset) / ds.scale
+        sigma[b["idx"]] = pipe.extract(pts).to(dtype=sigma.dtype) / ds.scale
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    prof = _lib.KernelTimer()
+    with prof:
+        for _ in range(args.profile_steps):
+            step()
+    kernels = {}
+    models = kernel_models(pipe, P)
+    models["field_fwd"] = dict(models["field_fwd"])
+    for name, st in sorted(prof.summary().items(), key=lambda kv: -kv[1]["total_ms"]):
+        e = {"avg_ms": round(st["avg_ms"], 4),
+             "ms_per_step": round(st["total_ms"] / args.profile_steps, 4)}
+        if name in models:
+            e.update(_roof(models[name], st["avg_ms"], peaks, "mfma_f16_tfs"))
+        kernels[name] = e
+    dominant = next((n for n in kernels if "bound" in kernels[n]), None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer = _lib.KernelTimer(only={dominant}) if dominant else None
+    t0 = time.perf_counter()
+    with (timer or _NullCtx()):
+        for _ in range(args.steps):
+            step()
+    t_host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms = elapsed / args.steps * 1e3
+    value = P * world * args.steps / elapsed
+    roofline = None
+    if timer:
+        st = timer.summary().get(dominant)
+        mdl = models[dominant]
+        r = _roof(mdl, st["avg_ms"], peaks, "mfma_f16_tfs")
+        if r["bound"] == "hbm":
+            ach, peak, frac, unit = r["hbm_gbs"], peaks["hbm_copy_gbs"], r["hbm_frac"], "GB/s"
+        else:
+            ach, peak, frac, unit = r["mfma_tfs"], peaks["mfma_f16_tfs"], r["mfma_frac"], "TFLOP/s"
+        roofline = {"kernel": dominant, "bound": r["bound"], "achieved": ach, "peak": peak,
+                    "unit": unit, "frac": frac, "traffic": None, "avg_ms": round(st["avg_ms"], 4),
+                    "launches": st["launches"], "units_per_launch": P,
+                    "algorithmic_bytes": mdl["bytes"], "algorithmic_flops": mdl["flops"],
+                    "bytes_per_unit": mdl["bytes"] / P,
+                    "ceiling": "HBM float4 copy, measured" if r["bound"] == "hbm"
+                    else "dense MFMA loop on random operands, measured"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline
+
+        cpu = cpu_baseline.run_extract(budget_s=min(args.cpu_budget, 20.0))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "extract points/sec", "value": round(value, 1), "unit": "points/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 4), "host_ms_per_step": round(t_host / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f16",
+            "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} HARP2-shaped "
+                    f"scene; extract grid {grid.shp[0]}x{grid.shp[1]} columns x {A} altitudes "
+                    f"= {len(grid)} points; random-init weights)",
+            "config": {"workload": f"extract (scripts/extract.py:180-211): batches of {cols} "
+                                   f"columns x {A} altitudes = {P} points, f64 preprocessor + "
+                                   f"hash grid + density MLP, forward only",
+                       "points_per_batch": P, "parallelism": f"dp{world}"},
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
+            "kernels_source": f"untimed profiling pass of {args.profile_steps} batches",
+            "peaks": peaks, "sigma_checksum": float(sigma.double().sum().item()),
+            "scene_build_s": round(t_scene, 2)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+class IngpJob:
+    """One Instant-NGP training job of the bench: pipeline, optimizer, flat gradient bucket
+    and rank-sharded loader, stepped eagerly or through a captured hipGraph of the whole
+    step (atmonr_amd.graph: one graph launch per step; the optimizer is in the graph on
+    one rank, and runs eagerly after the replay with its collectives on more)."""
+
+    def __init__(self, args, cfg, ds, dev, rank, world, rank_batch, numerics, graph, shard,
+                 occ):
+        from atmonr_amd.parallel import FlatGradBucket, ShardedAdam
+        from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
+
+        self.args, self.ds, self.dev, self.rank, self.world = args, ds, dev, rank, world
+        dtype = torch.float32 if args.dtype == "f32" else torch.float16
+        mlp_dtype = torch.bfloat16 if args.dtype == "bf16" else dtype
+        self.numerics = numerics
+        pipe = InstantNGPPipeline(cfg, ds, dtype=dtype, fused=True, seed=1337, occupancy=occ,
+                                  mlp_dtype=mlp_dtype, numerics=numerics)
+        pipe.send_tensors_to(dev)
+        opt_cfg = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
+        opt = pipe.get_optimizer(opt_cfg)
+        self.sharded = shard != "off"
+        self.shard = shard
+        # the AdamW update joins the graph only without collectives after backward
+        self.opt_in_graph = graph and not self.sharded and world == 1
+        opt.capturable = self.opt_in_graph
+        # one flat f32 gradient bucket; every param's .grad is a view into it, so backward
+        # accumulates in place and DP needs exactly one all-reduce per step
+        bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev,
+                                pad_to=world)
+        if world > 1:
+            bucket.broadcast_params(0)  # replicas start from rank 0's weights
+        if self.sharded:
+            opt = ShardedAdam(bucket, opt.param_groups, betas=opt_cfg["betas"],
+                              eps=opt_cfg["eps"], gather=shard)
+        elif not args.no_fused_zero:
+            bucket.fuse_zero_into(opt)  # the AdamW pass zeroes the bucket (no per-step fill)
+        if not args.no_overlap and not self.sharded and not (graph and world > 1):
+            # each chunk's all-reduce starts once its gradients are final: the surface and
+            # MLP gradients reduce while the hash-grid backward runs
+            bucket.enable_overlap()
+        self.pipe, self.opt, self.bucket = pipe, opt, bucket
+        self.set_batch(rank_batch, graph)
+
+    def _after(self):
+        if self.sharded:
+            return self.opt.step  # reduce-scatter, sharded AdamW, all-gather
+        bucket, opt = self.bucket, self.opt
+
+        def after():
+            bucket.all_reduce()
+            opt.step()
+        return after
+
+    def _graph(self, bs):
+        from atmonr_amd.graph import GraphedTrainStep
+
+        return GraphedTrainStep(self.pipe, self.ds, bs, self.opt, self.bucket,
+                                optimizer_in_graph=self.opt_in_graph,
+                                after=None if self.opt_in_graph else self._after())
+
+    def set_batch(self, bs: int, graph: bool) -> None:
+        from atmonr_amd.batch_loader import BatchLoader
+
+        if graph and self.world > 1 and self.bucket.overlap:
+            graph = False  # the overlapped all-reduce issues collectives inside backward
+        self.batch_size = bs
+        self.loader = BatchLoader(self.ds, bs, shuffle=True, rank=self.rank,
+                                  world_size=self.world, seed=0)
+        self._it = self.loader.index_batches()
+        self.graphed = graph
+        self.gstep = self._graph(bs) if graph else None
+        self._eager_left = 1 if graph else 0  # one eager step at the shape before capture
+
+    def next_idx(self):
+        try:
+            return next(self._it)
+        except StopIteration:
+            self._it = self.loader.index_batches()
+            return next(self._it)
+
+    def eager_step(self, idx=None):
+        idx = self.next_idx() if idx is None else idx
+        batch = self.ds.__getbatch__(idx)
+        res = self.pipe.forward(batch)
+        loss = self.pipe.compute_loss(batch, res)
+        self.bucket.zero()
+        loss.backward()
+        if not self.sharded:
+            self.bucket.all_reduce()
+        self.opt.step()  # ShardedAdam: reduce-scatter, sharded AdamW, all-gather
+        return loss
+
+    def step(self):
+        if self.gstep is None or self._eager_left > 0:
+            self._eager_left = max(0, self._eager_left - 1)
+            return self.eager_step()
+        return self.gstep(self.next_idx())
+
+    def profile(self, n, models, peaks, mfma_key) -> dict:
+        """Per-kernel table from ``n`` eager steps with events around every libanr call
+        (a graphed job's replays run the same kernels with the same arguments)."""
+        from atmonr_amd import _lib
+
+        prof = _lib.KernelTimer()
+        with prof:
+            for _ in range(n):
+                self.eager_step()
+        out = {}
+        for name, st in sorted(prof.summary().items(), key=lambda kv: -kv[1]["total_ms"]):
+            entry = {"avg_ms": round(st["avg_ms"], 4), "ms_per_step": round(st["total_ms"] / n, 4)}
+            mdl = models.get(name)
+            if mdl:
+                entry.update(_roof(mdl, st["avg_ms"], peaks, mfma_key))
+            out[name] = entry
+        return out
+
+    def time_dominant(self, name: str, n: int):
+        """Live duration of kernel ``name`` in graph replays: a second capture of the step
+        with timing events recorded as graph nodes around that kernel, replayed ``n``
+        times; each replay's pair is read after it completes. None if the runtime cannot
+        time events recorded inside a graph."""
+        from atmonr_amd import _lib
+
+        g = self._graph(self.batch_size)
+        timer = _lib.KernelTimer(only={name}, external=True)
+        try:
+            g.capture(self.next_idx(), timer=timer)
+            ts = []
+            for _ in range(n):
+                g(self.next_idx())
+                torch.cuda.synchronize()
+                ts += [a.elapsed_time(b) for a, b in timer.events.get(name, [])]
+        except (RuntimeError, _lib.ANRError) as e:  # noqa: BLE001
+            return {"error": str(e)[:200]}
+        finally:
+            del g
+        if not ts:
+            return None
+        return {"launches": len(ts), "total_ms": sum(ts), "avg_ms": sum(ts) / len(ts),
+                "source": "HIP events recorded inside the step's hipGraph around this kernel, "
+                          "read after each of the replays following the timed region"}
+
+    def release(self) -> None:
+        self.gstep = None
+        self.pipe = self.opt = self.bucket = None
+
+
 def _launch_ranks(n: int) -> int:
     """torch.distributed.run with N local ranks on this script (same arguments), as a
     child process: rendezvous on 127.0.0.1, one process per GPU."""
@@ -290,8 +561,12 @@ def main():
     ap.add_argument("--samples", type=int, default=1024)
     ap.add_argument("--views", type=int, default=90)
     ap.add_argument("--img-size", type=int, default=512)
-    ap.add_argument("--workload", choices=["ingp", "nerf"], default="ingp",
-                    help="ingp: BASELINE configs[2] (the headline line); nerf: configs[1]")
+    ap.add_argument("--workload", choices=["ingp", "nerf", "extract"], default="ingp",
+                    help="ingp: BASELINE configs[2] (the headline line); nerf: configs[1]; "
+                         "extract: the forward-only extract loop (SURVEY §8 f1), points/s")
+    ap.add_argument("--extract-batch", type=int, default=32768,
+                    help="extract: grid columns per batch (scripts/extract.py's batch_size; "
+                         "x 81 altitudes points)")
     ap.add_argument("--variant", choices=["baseline", "committed"], default="baseline")
     ap.add_argument("--dtype", choices=["f16", "bf16", "f32"], default="f16",
                     help="f16: tcnn precision (the reference's); bf16: BASELINE configs[4], "
@@ -310,11 +585,22 @@ def main():
                     help="zero the gradient bucket with a fill instead of in the AdamW pass")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one all-reduce of the whole gradient bucket after backward")
-    ap.add_argument("--shard-optimizer", choices=["off", "f16", "f32"], default="off",
+    ap.add_argument("--shard-optimizer", choices=["auto", "off", "f16", "f32"],
+                    default="auto",
                     help="ZeRO-1 (atmonr_amd.parallel.ShardedAdam): reduce-scatter of the "
                          "gradient, AdamW on 1/N of the parameters, all-gather of the f16 "
                          "compute copy (f16) or of the f32 parameters (f32), instead of "
-                         "all-reduce + replicated AdamW")
+                         "all-reduce + replicated AdamW; auto = f16 on more than one rank")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="replay the whole train step as one captured hipGraph "
+                         "(atmonr_amd.graph); auto = on for per-rank batches <= 2048 rays, "
+                         "where issuing ~50 launches from Python is slower than running them")
+    ap.add_argument("--numerics", choices=["build", "reference"], default="build",
+                    help="headline numerics of InstantNGPPipeline: build (f32 composite / "
+                         "loss / inter-kernel gradients) or reference (the reference's f16 "
+                         "composite, loss and loss-scaled tcnn backward: the PSNR-parity "
+                         "path); the other one is timed after it unless --no-alt-numerics")
+    ap.add_argument("--no-alt-numerics", action="store_true")
     ap.add_argument("--field-bwd", choices=["rt", "rt_lt", "lds"], default="rt",
                     help="fused field backward generation (anr_ingp_field_force_bwd): "
                          "register-transposed (default), the same with the dW operand "
@@ -359,6 +645,8 @@ def main():
     t_scene = time.time() - t0
     if args.workload == "nerf":
         return run_nerf(args, ds, dev, rank, world, t_scene)
+    if args.workload == "extract":
+        return run_extract(args, ds, dev, rank, world, t_scene)
     if args.global_batch:
         if args.global_batch % world:
             sys.exit(f"--global-batch {args.global_batch} is not divisible by {world} ranks")
@@ -366,60 +654,23 @@ def main():
     else:
         rank_batch, scaling = args.batch, "weak"
     cfg = ingp_config(args.variant, args.samples)
-    dtype = torch.float32 if args.dtype == "f32" else torch.float16
-    mlp_dtype = torch.bfloat16 if args.dtype == "bf16" else dtype
     occ = None
     if args.occupancy:
         from atmonr_amd.occupancy import OccupancyGrid
 
         occ = OccupancyGrid((128, 128, 32), alt_compress=float(cfg["alt_compress_factor"]),
                             warmup=args.occ_warmup, update_every=16, device=dev)
-    pipe = InstantNGPPipeline(cfg, ds, dtype=dtype, fused=True, seed=1337, occupancy=occ,
-                              mlp_dtype=mlp_dtype)
-    pipe.send_tensors_to(dev)
-    opt_cfg = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
-    opt = pipe.get_optimizer(opt_cfg)
-
-    # one flat f32 gradient bucket; every param's .grad is a view into it, so backward
-    # accumulates in place and DP needs exactly one all-reduce per step
-    from atmonr_amd.parallel import FlatGradBucket, ShardedAdam
-
-    sharded = args.shard_optimizer != "off"
-    bucket = FlatGradBucket([p for g in opt.param_groups for p in g["params"]], dev,
-                            pad_to=world)
-    if world > 1:
-        bucket.broadcast_params(0)  # replicas start from rank 0's weights
-    if sharded:
-        opt = ShardedAdam(bucket, opt.param_groups, betas=opt_cfg["betas"], eps=opt_cfg["eps"],
-                          gather=args.shard_optimizer)
-    elif not args.no_fused_zero:
-        bucket.fuse_zero_into(opt)  # the AdamW pass zeroes the bucket (no per-step fill)
-    if not args.no_overlap and not sharded:
-        # each chunk's all-reduce starts once its gradients are final: the surface and MLP
-        # gradients reduce while the hash-grid backward runs
-        bucket.enable_overlap()
-
-    loader = BatchLoader(ds, rank_batch, shuffle=True, rank=rank, world_size=world, seed=0)
-    it = iter(loader)
-
-    def next_batch():
-        nonlocal it
-        try:
-            return next(it)
-        except StopIteration:
-            it = iter(loader)
-            return next(it)
-
-    def step():
-        batch = next_batch()
-        res = pipe.forward(batch)
-        loss = pipe.compute_loss(batch, res)
-        bucket.zero()
-        loss.backward()
-        if not sharded:
-            bucket.all_reduce()
-        opt.step()  # ShardedAdam: reduce-scatter, sharded AdamW, all-gather
-        return loss
+    shard = args.shard_optimizer
+    if shard == "auto":  # ZeRO-1 with the f16 all-gather on more than one rank
+        shard = "f16" if world > 1 else "off"
+    use_graph = {"on": True, "off": False}.get(args.graph, rank_batch <= 2048)
+    if occ is not None:
+        use_graph = False  # the occupancy grid's refresh and compaction sizes are dynamic
+    job = IngpJob(args, cfg, ds, dev, rank, world, rank_batch, args.numerics, use_graph,
+                  shard, occ)
+    pipe, bucket, opt = job.pipe, job.bucket, job.opt
+    sharded = job.sharded
+    step = job.step
 
     for _ in range(args.warmup):
         loss = step()
@@ -430,7 +681,8 @@ def main():
 
     # Untimed profiling pass: HIP events around every libanr call give the per-kernel
     # breakdown and pick the dominant kernel; the timed region below then brackets only
-    # that kernel's launches (events around every call would cost ~0.2 ms per step).
+    # that kernel's launches (events around every call would cost ~0.2 ms per step). A
+    # graphed job profiles its eager form (the same kernels and arguments).
     M = rank_batch * args.samples
     peaks = measured_peaks(dev, args.spec_peaks)
     mfma_key = {"f32": "mfma_f32_tfs", "bf16": "mfma_bf16_tfs"}.get(args.dtype, "mfma_f16_tfs")
@@ -446,25 +698,16 @@ def main():
     models = kernel_models(pipe, M, pmc, pmc_sfx)
     kernels, dominant = {}, None
     if not args.no_kernel_timer:
-        prof = _lib.KernelTimer()
-        with prof:
-            for _ in range(args.profile_steps):
-                loss = step()
-        summ = prof.summary()
-        for name, st in sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"]):
-            entry = {"avg_ms": round(st["avg_ms"], 4),
-                     "ms_per_step": round(st["total_ms"] / args.profile_steps, 4)}
-            mdl = models.get(name)
-            if mdl:
-                entry.update(_roof(mdl, st["avg_ms"], peaks, mfma_key))
-            kernels[name] = entry
+        kernels = job.profile(args.profile_steps, models, peaks, mfma_key)
         dominant = next((n for n in kernels if "bound" in kernels[n]), None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
-    timer = _lib.KernelTimer(only={dominant}) if dominant else None
+    # graphed steps cannot carry events per launch: their dominant kernel is timed by
+    # job.time_dominant after the timed region (events recorded inside the graph)
+    timer = _lib.KernelTimer(only={dominant}) if dominant and not job.graphed else None
     t_start = time.perf_counter()
     if timer:
         with timer:
@@ -488,35 +731,67 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     rays_total = rank_batch * world * args.steps
     value = rays_total / elapsed
+    dom_stats = None
+    if timer:
+        dom_stats = timer.summary().get(dominant)
+    elif dominant and job.graphed:
+        dom_stats = job.time_dominant(dominant, args.steps)
 
     strong = None
     if world > 1 and scaling == "weak" and not args.no_strong and args.batch % world == 0:
         # the same job at a fixed global batch of --batch rays (SURVEY §8(e)'s strong-
         # scaling target), timed the same way after a short warm-up at the new shape
-        loader = BatchLoader(ds, args.batch // world, shuffle=True, rank=rank,
-                             world_size=world, seed=0)
-        it = iter(loader)
+        sb = args.batch // world
+        job.set_batch(sb, {"on": True, "off": False}.get(args.graph, sb <= 2048)
+                      and occ is None)
         for _ in range(max(2, args.warmup)):
-            step()
+            job.step()
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            job.step()
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         t = torch.tensor([time.perf_counter() - t1], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
-        strong = {"global_batch": args.batch, "per_rank_batch": args.batch // world,
+        strong = {"global_batch": args.batch, "per_rank_batch": sb, "graph": job.graphed,
                   "value": round(args.batch * args.steps / el, 1),
                   "ms_per_step": round(el / args.steps * 1e3, 3), "steps": args.steps}
 
+    # the other numerics of the same workload, timed the same way (one rank): the
+    # reference's f16 composite / loss / loss-scaled backward (numerics="reference", the
+    # PSNR-parity path) beside the build numerics, or the other way round
+    alt = None
+    if world == 1 and not args.no_alt_numerics and occ is None and args.dtype == "f16":
+        other = "reference" if args.numerics == "build" else "build"
+        del step
+        job.release()
+        torch.cuda.empty_cache()
+        ajob = IngpJob(args, cfg, ds, dev, rank, world, rank_batch, other, use_graph, shard,
+                       None)
+        for _ in range(args.warmup):
+            ajob.step()
+        akern = ajob.profile(args.profile_steps, kernel_models(ajob.pipe, M), peaks, mfma_key)
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            aloss = ajob.step()
+        torch.cuda.synchronize()
+        ea = time.perf_counter() - ta
+        alt = {"numerics": other, "value": round(rank_batch * args.steps / ea, 1),
+               "ms_per_step": round(ea / args.steps * 1e3, 3), "graph": ajob.graphed,
+               "final_loss": round(float(aloss.item()), 6),
+               "kernels": {k: {x: v[x] for x in ("avg_ms", "ms_per_step") if x in v}
+                           for k, v in akern.items()}}
+        ajob.release()
+
     roofline = None
-    if timer:
-        st = timer.summary().get(dominant)
+    if dom_stats:
+        st = dom_stats
         if st:  # the dominant kernel, timed live over the timed region
             mdl = models[dominant]
             k = _roof(mdl, st["avg_ms"], peaks, mfma_key)
@@ -588,6 +863,8 @@ def main():
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
+            "numerics": args.numerics,
+            "graph": job.graphed,
             "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} "
                     f"HARP2-shaped scene, {len(ds)} rays; random-init weights)",
             "config": {
@@ -608,6 +885,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "strong_scaling": strong,
+            "alt_numerics": alt,
             "peaks": peaks,
             "kernels": kernels,
             "kernels_source": f"untimed profiling pass of {args.profile_steps} steps",
@@ -618,8 +896,8 @@ def main():
                 "backend": dist.get_backend() if world > 1 else None},
             "sharded_optimizer": None if not sharded else {
                 "reduce_scatter_bytes": 4 * bucket.numel,
-                "all_gather_bytes": (2 if args.shard_optimizer == "f16" else 4) * bucket.numel,
-                "state_floats_per_rank": opt.state_numel(), "gather": args.shard_optimizer,
+                "all_gather_bytes": (2 if shard == "f16" else 4) * bucket.numel,
+                "state_floats_per_rank": opt.state_numel(), "gather": shard,
                 "backend": dist.get_backend() if world > 1 else None},
             "occupancy": None if occ is None else {
                 "grid": list(occ.res), "threshold": occ.threshold, "warmup": occ.warmup,

@@ -537,6 +537,21 @@ int anr_adam_step_multi(const anr_adam_tensor* tensors, int32_t n_tensors, float
                         float beta2, float eps, int32_t decoupled, int32_t zero_grad,
                         anr_stream_t stream);
 
+/* anr_adam_step_multi with the step count and the learning rates in DEVICE memory, so
+ * that one captured launch serves every replay of a hipGraph of the train step
+ * (torch.optim.AdamW(capturable=True) keeps its step on the device for the same reason;
+ * trainer.py:105 is the call site). Per call: *d_step += 1 on the device, then every
+ * tensor t is updated with step = *d_step and lr = d_lr[t] (the descriptors' lr and
+ * step fields are ignored; weight_decay and the pointers are taken from them at the
+ * call). d_scratch: 3 * ANR_ADAM_DEV_MAX_TENSORS floats of caller-owned device memory
+ * (the per-tensor bias-corrected scalars). At most ANR_ADAM_DEV_MAX_TENSORS tensors.
+ * Same arithmetic as anr_adam_step_multi (bias corrections in double). */
+#define ANR_ADAM_DEV_MAX_TENSORS 64
+int anr_adam_step_multi_dev(const anr_adam_tensor* tensors, int32_t n_tensors, float beta1,
+                            float beta2, float eps, int32_t decoupled, int32_t zero_grad,
+                            int64_t* d_step, const float* d_lr, float* d_scratch,
+                            anr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

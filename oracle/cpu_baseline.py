@@ -71,6 +71,66 @@ def run(budget_s: float = 40.0, batch_size: int = 1024, threads: int | None = No
     }
 
 
+def run_extract(budget_s: float = 20.0, n_points: int = 131072, threads: int | None = None,
+                seed: int = 0, timed: int = 3) -> dict:
+    """Points/s of the extract loop body (scripts/extract.py:203-209 ->
+    instant_ngp.py:208-247) restated on the CPU: (xyz - offset) / scale in f64, the
+    horizontal preprocessor in f64 torch (ref_nerf.preprocess_torch), the INGP remap,
+    the restated tcnn hash grid (numpy, f16 table) and the f16-rounded pos MLP
+    (ref_tcnn), relu of output 0, / scale. Median of ``timed`` batches of ``n_points``
+    random in-scene points (stops early at ``budget_s``)."""
+    from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
+    from oracle import ref_nerf, ref_tcnn
+
+    if threads is None:
+        env = os.environ.get("OMP_NUM_THREADS", "")
+        threads = int(env) if env.isdigit() and int(env) > 0 else min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    gen = torch.Generator().manual_seed(seed)
+    ds = SyntheticHARP2Dataset(n_views=8, img_size=64, device="cpu", seed=seed)
+    pp = ds._prep
+    offset = torch.tensor(pp.offset, dtype=torch.float64)
+    cfg = (3, 16, 16, 1.3819, 19)
+    n_table = int(ref_tcnn.grid_levels(3, 16, 16, 1.3819, 19)[4]) * 2
+    table = ((torch.rand(n_table, generator=gen, dtype=torch.float64) * 2 - 1) * 1e-4
+             ).half().double().numpy()
+    w = (torch.rand(32 * 64 + 64 * 16, generator=gen, dtype=torch.float64) - 0.5) * 0.3
+    pts_n = (torch.rand(n_points, 3, generator=gen, dtype=torch.float64) * 2 - 1) * torch.tensor(
+        [0.9, 0.9, 0.2], dtype=torch.float64)
+    xyz = pts_n * ds.scale + offset
+
+    def body():
+        pts = (xyz - offset) / ds.scale
+        c = ref_nerf.preprocess_torch(pts, scale=float(pp.scale), offset=offset,
+                                      lat_min=pp.lat_min, lat_range=pp.lat_range,
+                                      lon_min=pp.lon_min, lon_range=pp.lon_range,
+                                      h0=pp.ray_origin_height, shift_lon=pp.shift_lon)
+        c = (c + 1) / 2
+        c[..., 2] = c[..., 2] / 8.0
+        enc = torch.from_numpy(ref_tcnn.hashgrid_fwd(c.float().double().numpy(), table, cfg))
+        out = ref_tcnn.mlp_fwd(enc, w, 32, 16, 64, 1, half=True)
+        return torch.clip(out[:, :1], min=0) / ds.scale
+
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        body()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start >= budget_s or len(times) >= timed:
+            break
+    times.sort()
+    med = times[len(times) // 2]
+    return {
+        "value": n_points / med, "unit": "points/s", "cores": threads,
+        "host_cpus": os.cpu_count(), "kind": "port",
+        "sample": (f"extract loop body (f64 preprocessor, tcnn hash grid T=2^19 and 2x64 "
+                   f"pos MLP restated in numpy / torch CPU) on {n_points} random in-scene "
+                   f"points, median of {len(times)} batches, {threads} threads of "
+                   f"{os.cpu_count()} host CPUs"),
+    }
+
+
 if __name__ == "__main__":
     import sys
 

@@ -91,3 +91,44 @@ def test_extract_volume_loop(scene, dev):
     grid.dump(path, sigma)
     d = np.load(path)
     assert d["extinction"].shape == (48, 48, A, 1) and d["sample_alt"].shape == (A,)
+
+
+def test_extract_full_batch_spot_rows(scene, dev):
+    """scripts/extract.py's batch shape: 32,768 columns x 81 altitudes (250 m steps to
+    20 km) = 2,654,208 points in ONE pipeline.extract call (the bench's extract step).
+    4,096 spot rows spread over the batch against the oracle (f64 preprocessor, restated
+    tcnn hash grid, f16-rounded pos MLP), tolerance 1e-2 of the largest value (f16
+    kernels); the batched loop equals one call over the whole grid."""
+    from atmonr_amd.extract import GridExtractDataset, extract_volume
+    from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
+    from oracle import ref_tcnn
+
+    p = InstantNGPPipeline(ge._ingp_config(64), scene, seed=9)
+    p.send_tensors_to(dev)
+    p.eval()
+    # a 256 x 128 lat/lon grid across the scene's footprint (the L1C grid stand-in)
+    lat0, lon0 = scene.lat.min().item(), scene.lon.min().item()
+    lat1, lon1 = scene.lat.max().item(), scene.lon.max().item()
+    lat = torch.linspace(lat0, lat1, 256, device=dev)[:, None].expand(256, 128).contiguous()
+    lon = torch.linspace(lon0, lon1, 128, device=dev)[None, :].expand(256, 128).contiguous()
+    grid = GridExtractDataset(scene, alt_step=250.0, lat=lat, lon=lon)
+    A = grid.sample_alt.shape[0]
+    assert A == 81 and len(grid) == 32768 * 81
+    sigma = extract_volume(p, scene, grid, batch_size=32768)
+    halves = extract_volume(p, scene, grid, batch_size=16384)
+    assert torch.equal(sigma, halves)
+    gen = torch.Generator().manual_seed(3)
+    rows = torch.randint(0, len(grid), (4096,), generator=gen)
+    pts = (grid.xyz[rows.to(dev)] - torch.as_tensor(scene.offset, dtype=torch.float64,
+                                                     device=dev)) / scene.scale
+    coords = _oracle_coords_f64(pts.cpu(), scene.get_point_preprocessor("horizontal"))
+    table = p.pos_encoder.params.detach().half().double().cpu().numpy()
+    enc = torch.from_numpy(ref_tcnn.hashgrid_fwd(coords.double().numpy(), table,
+                                                 (3, 16, 16, 1.3819, 19)))
+    pos_out = ref_tcnn.mlp_fwd(enc.half().double(), p.pos_mlp.params.detach().double().cpu(),
+                               32, 16, p.pos_mlp.width, 1, half=True)
+    ref_sigma = torch.clip(pos_out[:, :1], min=0) / scene.scale
+    got = sigma[rows.to(dev)].double().cpu()
+    err = (got - ref_sigma).abs().max().item()
+    assert err <= 1e-2 * ref_sigma.abs().max().item() + 1e-12, err
+    assert (ref_sigma > 0).any()

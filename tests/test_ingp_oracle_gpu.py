@@ -317,25 +317,32 @@ class _ReferenceRunner:
 
 
 @pytest.mark.timeout(1200)
-def test_psnr_vs_reference_semantics(scene, dev):
-    """PSNR at 0/8/16/32/64 iterations (8 epochs of the 8-view 16x16 scene): the pipeline
-    in reference numerics, the pipeline in build numerics and the oracle in reference
-    semantics train side by side on the same batches and draws (tests/ingp_psnr.py).
-    Reference numerics must stay within 0.1 dB of the oracle at every checkpoint (the
-    north-star PSNR bar). The build numerics' distance is recorded beside it; the oracle's
-    own spread under one-rounding perturbations is measured separately on the CPU
+@pytest.mark.parametrize("n_samples,batch,checkpoints", [
+    (N, 256, (0, 8, 16, 32, 64)),
+    # BASELINE configs[2]'s 1,024 samples per ray, where the reference's f16 composite
+    # underflows hardest: 64 rays per step, 2 epochs of the scene
+    (1024, 64, (0, 8, 64))])
+def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
+    """PSNR at fixed iterations: the pipeline in reference numerics, the pipeline in build
+    numerics and the oracle in reference semantics train side by side on the same batches
+    and draws (tests/ingp_psnr.py), at 64 samples per ray (8 epochs of the 8-view 16x16
+    scene) and at the bench's 1,024. Reference numerics must stay within 0.1 dB of the
+    oracle at every checkpoint (the north-star PSNR bar). The build numerics' distance is
+    recorded beside it (a deliberate deviation: DESIGN.md §3.1); the oracle's own spread
+    under one-rounding perturbations is measured separately on the CPU
     (tools/ingp_oracle_spread.py, profiles/r03_ingp_oracle_spread.json)."""
     from tests.ingp_psnr import PipelineRunner, train_side_by_side
 
-    p_ref, o = _pair(scene, dev, torch.float16, numerics="reference")
-    p_build, _ = _pair(scene, dev, torch.float16)
+    p_ref, o = _pair(scene, dev, torch.float16, numerics="reference", n_samples=n_samples)
+    p_build, _ = _pair(scene, dev, torch.float16, n_samples=n_samples)
     for m in ref_ingp.MODULES:  # same initial parameters (seed 5) for both pipelines
         assert torch.equal(getattr(p_ref, m).params, getattr(p_build, m).params)
     runners = {"gpu_reference_numerics": PipelineRunner(p_ref, OPT, dev),
                "gpu_build": PipelineRunner(p_build, OPT, dev),
                "oracle_reference_semantics": _ReferenceRunner(o)}
-    out = train_side_by_side(runners, scene, N, progress=lambda r: (_REC.update(
-        psnr_reference_semantics=r), _dump()))
+    key = "psnr_reference_semantics" + ("" if n_samples == N else f"_n{n_samples}")
+    out = train_side_by_side(runners, scene, n_samples, checkpoints=checkpoints, batch=batch,
+                             progress=lambda r: (_REC.update({key: r}), _dump()))
     rows = []
     for i, r in enumerate(out["oracle_reference_semantics"]):
         row = {"iteration": r["iteration"], "psnr_oracle": r["psnr"],
@@ -344,10 +351,10 @@ def test_psnr_vs_reference_semantics(scene, dev):
         row["delta_reference_numerics_db"] = row["psnr_gpu_reference_numerics"] - r["psnr"]
         row["delta_build_db"] = row["psnr_gpu_build"] - r["psnr"]
         rows.append(row)
-    _REC["psnr_reference_semantics"] = rows
-    _REC["zero_rays"] = int(p_ref._zero_rays.item())
+    _REC[key] = rows
+    _REC["zero_rays" + key[len("psnr_reference_semantics"):]] = zr = p_ref.zero_rays_total
     _dump()
-    assert _REC["zero_rays"] == 0
+    assert zr == 0
     for row in rows:
         assert abs(row["delta_reference_numerics_db"]) <= 0.1, rows
-    assert rows[-1]["psnr_oracle"] > rows[0]["psnr_oracle"] + 3.0, rows
+    assert rows[-1]["psnr_oracle"] > rows[0]["psnr_oracle"] + 1.0, rows

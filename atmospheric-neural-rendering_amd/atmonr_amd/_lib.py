@@ -220,11 +220,6 @@ _SIGNATURES = {
         [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64,
          _P, _P, c_int64, _P, c_int64, _P, _P, _P, c_int64, _P],
     ),
-    "anr_ingp_field_bwd_tm": (
-        c_int32,
-        [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64,
-         _P, _P, c_int64, _P, _P, c_int64, _P, _P, _P],
-    ),
     "anr_ingp_field_fwd_rows": (
         c_int32,
         [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64,
@@ -251,12 +246,6 @@ _SIGNATURES = {
         [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, c_int32,
          _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
-    "anr_composite_bwd_tm": (
-        c_int32,
-        [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, c_int32,
-         _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
-    ),
-    "anr_composite_tile_max_supported": (c_int32, [c_int32, c_int32, c_int32, c_int32]),
     "anr_loss_workspace_bytes": (c_int64, [c_int64]),
     "anr_loss_fwd_bwd": (
         c_int32,

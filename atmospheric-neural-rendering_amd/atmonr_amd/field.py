@@ -35,7 +35,6 @@ import torch
 
 from . import _lib
 from ._lib import call, dtype_code, ptr
-from .graphics_utils import take_tile_max
 
 
 _grad_target = _lib.grad_target
@@ -183,19 +182,9 @@ class IngpFieldFn(torch.autograd.Function):
                  ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), float(ls), s,
                  tag="field_bwd")
         else:
-            # the composite backward's per-tile maxima of exactly these gradients, if it
-            # left them (graphics_utils.take_tile_max): no separate max pass over them
-            tm = take_tile_max(d_color, d_sigma)
-            tm = tm if ctx.rows is None else None
             ws_bytes = _lib.load().anr_ingp_field_bwd_workspace_bytes(pdesc, ddesc, mma, M)
-            ws = None if tm is not None else torch.empty(max(1, -(-ws_bytes // 4)), device=dev,
-                                                         dtype=torch.float32)
-            if tm is not None:
-                call("anr_ingp_field_bwd_tm", pdesc, ddesc, mma, ptr(packed), ptr(enc),
-                     enc.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
-                     d_color.stride(0), ptr(tm), ptr(d_enc), d_enc.stride(0), ptr(g_pos),
-                     ptr(g_dir), s, tag="field_bwd")
-            elif ctx.rows is None:
+            ws = torch.empty(max(1, -(-ws_bytes // 4)), device=dev, dtype=torch.float32)
+            if ctx.rows is None:
                 call("anr_ingp_field_bwd", pdesc, ddesc, mma, ptr(packed), ptr(enc),
                      enc.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
                      d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),

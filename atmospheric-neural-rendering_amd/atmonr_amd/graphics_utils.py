@@ -9,50 +9,10 @@ have ``color.dtype`` as in the reference (graphics_utils.py:28).
 
 from __future__ import annotations
 
-import os
-import weakref
-
 import torch
 
 from . import _lib
 from ._lib import ANRError, call, dtype_code, ptr
-
-
-# Per-32-row maxima of |dL/dcolor|, |dL/dsigma| handed from the composite backward to the
-# fused field backward (anr_composite_bwd_tm -> anr_ingp_field_bwd_tm: the f16 gradient
-# scale's input without a separate reduction pass). One slot per device, holding weak
-# references to the gradient tensors: while one is alive its memory cannot belong to
-# another tensor, so the field takes the maxima only for the same live storage at the
-# same version (autograd passes the composite's outputs on as views; an in-place
-# accumulation bumps the shared version, a summed or converted gradient is a new tensor).
-_TILE_MAX: dict = {}
-# Opt-in (ANR_TILE_MAX=1). In the bench step it is neutral: the 30 us max pass it removes
-# ran beside the side-stream surface backward, which then contends with the hash-grid
-# backward instead (same-box A/B 3.200 vs 3.218 ms/step, traces 3.210 vs 3.177 ms;
-# profiles/r03_tile_max_ab.md).
-_TILE_MAX_ON = os.environ.get("ANR_TILE_MAX", "0") == "1"
-
-
-def _publish_tile_max(d_color: torch.Tensor, d_sigma: torch.Tensor, tm: torch.Tensor) -> None:
-    _TILE_MAX[d_color.device] = (weakref.ref(d_color), weakref.ref(d_sigma), d_color._version,
-                                 d_sigma._version, tm)
-
-
-def take_tile_max(d_color: torch.Tensor, d_sigma: torch.Tensor | None):
-    """The composite's per-tile maxima for exactly these gradients (consumed), else None."""
-    e = _TILE_MAX.pop(d_color.device, None)
-    if e is None or d_sigma is None:
-        return None
-    c0, s0, vc, vs, tm = e[0](), e[1](), e[2], e[3], e[4]
-    if c0 is None or s0 is None:
-        return None
-    same = (d_color.data_ptr() == c0.data_ptr() and d_sigma.data_ptr() == s0.data_ptr()
-            and d_color.numel() == c0.numel() and d_sigma.numel() == s0.numel()
-            and d_color.dtype == c0.dtype == torch.float32 and d_sigma.dtype == torch.float32
-            and d_color.is_contiguous() and d_sigma.is_contiguous()
-            and d_color._version == vc and d_sigma._version == vs
-            and c0._version == vc and s0._version == vs)
-    return tm if same else None
 
 
 class _CompositeFn(torch.autograd.Function):
@@ -112,13 +72,7 @@ class _CompositeFn(torch.autograd.Function):
         args = (ptr(zc), ctx.z_scale, ptr(color), ptr(sigma), ptr(cs), dtype_code(dt), B, N, C,
                 S, ptr(prep(g_cm)), ptr(prep(g_atmo)), ptr(prep(g_surf)), ptr(prep(g_w)),
                 ptr(prep(g_alpha)), ptr(d_color), ptr(d_sigma), ptr(d_cs), ptr(d_z))
-        if (_TILE_MAX_ON and d_color is not None and d_sigma is not None
-                and _lib.load().anr_composite_tile_max_supported(dtype_code(dt), N, C, S)):
-            tm = torch.empty(B * N // 32, device=dev, dtype=torch.float32)
-            call("anr_composite_bwd_tm", *args, ptr(tm), _lib.stream(dev))
-            _publish_tile_max(d_color, d_sigma, tm)
-        else:
-            call("anr_composite_bwd", *args, _lib.stream(dev))
+        call("anr_composite_bwd", *args, _lib.stream(dev))
         if d_z is not None:
             d_z = d_z.to(ctx.z_dtype)
         return d_z, d_color, d_sigma, d_cs, None, None

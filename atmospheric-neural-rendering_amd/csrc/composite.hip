@@ -93,9 +93,6 @@ struct CompArgs {
   const void *d_color_map, *d_atmo, *d_surf, *d_weights, *d_alpha;
   void *d_color, *d_sigma, *d_color_surf;
   float* d_z;
-  // nullable (rb::bwd_kernel, T = float, S = 1, N % 32 == 0, 32 % SPL == 0): per 32 rays-
-  // major rows, the max of |d_color| (all C) and |d_sigma| written
-  float* tile_max;
 };
 
 // delta_i for sample i of a ray (graphics_utils.py:30-34), z already in the ray's row.
@@ -640,7 +637,6 @@ __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
       r[S == 1 ? 0 : c] += ldv(static_cast<const T*>(a.color_surf), b * C + c) * gs[c];
   }
   float dD[SPL];
-  float tmax = 0.0f;  // max |d_color|, |d_sigma| over this lane's samples (tile_max)
   T* dcol = a.d_color ? static_cast<T*>(a.d_color) + (b * N + i0) * C : nullptr;
   T* dsig = a.d_sigma ? static_cast<T*>(a.d_sigma) + (b * N + i0) * S : nullptr;
 #pragma unroll
@@ -657,14 +653,12 @@ __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
         for (int c = 0; c < C; ++c)
           if (S == 1 || c == s) {
             dcol[j * C + c] = from_f32<T>(w * ga[c]);
-            tmax = fmaxf(tmax, fabsf(w * ga[c]));
           }
       }
       float dal = Ti * (q[o] - V[s]) - r[s] * Pi * Q[s];
       if (a.d_alpha && j < nvalid) dal += ldv(static_cast<const T*>(a.d_alpha), (b * N + i0 + j) * S + s);
       if (dsig && j < nvalid) {
         dsig[j * S + s] = from_f32<T>(dal * e[o] * dl[j]);
-        tmax = fmaxf(tmax, fabsf(dal * e[o] * dl[j]));
       }
       dd += dal * e[o] * sg[o];
       const float t = (1.0f - al[o]) + (j < nvalid ? 1e-10f : 0.0f);
@@ -677,14 +671,6 @@ __global__ void __launch_bounds__(256) bwd_kernel(CompArgs a) {
 #pragma unroll
     for (int c = 0; c < C; ++c)
       static_cast<T*>(a.d_color_surf)[b * C + c] = from_f32<T>(Stot[S == 1 ? 0 : c] * gs[c]);
-  }
-  if constexpr (32 % SPL == 0) {
-    if (a.tile_max) {  // uniform; a 32-row tile = 32 / SPL consecutive lanes of one ray
-      constexpr int G = 32 / SPL;
-#pragma unroll
-      for (int o = 1; o < G; o <<= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
-      if ((lane & (G - 1)) == 0 && nvalid > 0) a.tile_max[(b * N + i0) / 32] = tmax;
-    }
   }
   if (a.d_z) {
     float dprev = shfl_up(dD[SPL - 1], 1);
@@ -786,51 +772,6 @@ extern "C" int anr_composite_fwd(const float* z, float z_scale, const void* colo
   else
     hipLaunchKernelGGL(composite_fwd_kernel<float>, grid, block, 0, as_stream(stream), a);
   ANR_CHECK_LAUNCH("anr_composite_fwd");
-  return ANR_OK;
-}
-
-namespace anr {
-// anr_composite_bwd_tm's shapes: launch_rb's register-blocked kernels with f32 io, S = 1,
-// rays a whole number of 32-row tiles and a lane's SPL samples dividing a tile
-static bool tile_max_ok(int32_t io_dtype, int32_t N, int32_t C, int32_t S) {
-  if (io_dtype != ANR_F32 || C != 4 || S != 1 || N < 32 || N % 32 != 0) return false;
-  const int spl = N <= 256 ? (N + 63) / 64 : (N + 255) / 256;
-  if (N > 256 && spl != 2 && spl != 4 && spl != 8 && spl != 16) return false;
-  return 32 % spl == 0 && !g_composite_generic;
-}
-}  // namespace anr
-
-extern "C" int anr_composite_tile_max_supported(int32_t io_dtype, int32_t N, int32_t C,
-                                                int32_t S) {
-  return anr::tile_max_ok(io_dtype, N, C, S) ? 1 : 0;
-}
-
-extern "C" int anr_composite_bwd_tm(const float* z, float z_scale, const void* color,
-                                    const void* sigma, const void* color_surf, int32_t io_dtype,
-                                    int64_t B, int32_t N, int32_t C, int32_t S,
-                                    const void* d_color_map, const void* d_atmo,
-                                    const void* d_surf, const void* d_weights,
-                                    const void* d_alpha, void* d_color, void* d_sigma,
-                                    void* d_color_surf, float* d_z, float* tile_max,
-                                    anr_stream_t stream) {
-  using namespace anr;
-  if (B == 0) return ANR_OK;
-  ANR_CHECK_ARG(z && color && sigma && d_color && d_sigma && tile_max,
-                "anr_composite_bwd_tm: null argument");
-  ANR_CHECK_ARG(B > 0 && tile_max_ok(io_dtype, N, C, S),
-                "anr_composite_bwd_tm: unsupported shape (N=%d C=%d S=%d)", N, C, S);
-  ANR_CHECK_ARG(d_color_surf == nullptr || color_surf != nullptr,
-                "anr_composite_bwd_tm: d_color_surf without color_surf");
-  CompArgs a{};
-  a.z = z; a.z_scale = z_scale; a.color = color; a.sigma = sigma; a.color_surf = color_surf;
-  a.B = B; a.N = N; a.C = C; a.S = S;
-  a.d_color_map = d_color_map; a.d_atmo = d_atmo; a.d_surf = d_surf;
-  a.d_weights = d_weights; a.d_alpha = d_alpha;
-  a.d_color = d_color; a.d_sigma = d_sigma; a.d_color_surf = d_color_surf; a.d_z = d_z;
-  a.tile_max = tile_max;
-  ANR_CHECK_ARG(launch_rb<float>(true, a, as_stream(stream)),
-                "anr_composite_bwd_tm: no register-blocked kernel for N=%d", N);
-  ANR_CHECK_LAUNCH("anr_composite_bwd_tm");
   return ANR_OK;
 }
 

@@ -271,10 +271,6 @@ struct Args {
   // > 0: reference numerics (tcnn's loss-scaled f16 backward, anr_ingp_field_bwd_ref16):
   // fixed gradient scale, f16 module-boundary gradients; 0: per-wavefront dynamic scale
   float loss_scale;
-  // nullable: tile_max[t] = max over rows [32t, 32t + 32) of |d_color[r][0..n_out)| and
-  // |d_sigma[r]|, written by the composite backward that produced them
-  // (anr_composite_bwd_tm); replaces absmax_kernel's pass over d_color / d_sigma
-  const float* tile_max;
 };
 
 // ROWS is a compile-time choice: a run-time test on a.rows in the prefetch paths put a
@@ -708,18 +704,12 @@ __device__ __forceinline__ void st4g(_Float16* base, int ld, int mrow, int col, 
   *reinterpret_cast<h4*>(base + mrow * ld + col) = v;
 }
 
-// The f16 gradient scale's input for a wavefront with tiles [t_begin, t_end): the max of
-// the composite's per-tile maxima when given (every lane reads a few, then a wave
-// reduction), else absmax_kernel's value. max is exact: both give the same float.
+// The f16 gradient scale's input for a wavefront with tiles [t_begin, t_end):
+// absmax_kernel's value (0 for a wavefront without rows).
 __device__ __forceinline__ float wave_grad_max(const Args& a, const float* wmax, int64_t w_id,
                                                int64_t t_begin, int64_t t_end) {
-  if (t_begin >= t_end) return 0.0f;
-  if (a.tile_max == nullptr) return wmax[w_id];
-  float m = 0.0f;
-  for (int64_t t = t_begin + (threadIdx.x & 63); t < t_end; t += 64) m = fmaxf(m, a.tile_max[t]);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
+  (void)a;
+  return t_begin >= t_end ? 0.0f : wmax[w_id];
 }
 
 // Rows of the backward's wavefront w: tiles [w*tpw, (w+1)*tpw) of 32 rows. The f16
@@ -1719,12 +1709,11 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
                       (mode == 2 ? 4 * 2 * kLtRegion * kLtSlot : 0)) * 2;
   if (lds > 160 * 1024) return 1;
   const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast, mode);
-  if (!BF && a.tile_max == nullptr &&
-      (ws == nullptr || ws_bytes < static_cast<int64_t>(sizeof(float)) * gm.nw))
+  if (!BF && (ws == nullptr || ws_bytes < static_cast<int64_t>(sizeof(float)) * gm.nw))
     return 2;
   const float target = ldexpf(1.0f, g_target_log2);
   const dim3 grid(static_cast<unsigned>(gm.blocks)), block(64 * waves);
-  if (!BF && a.tile_max == nullptr) {
+  if (!BF) {
     if (a.rows)
       hipLaunchKernelGGL(absmax_kernel<true>, dim3(gm.nw), dim3(1024), 0, st, a, gm.tpw * 32, ws);
     else
@@ -1912,11 +1901,8 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
                      int64_t n_per_ray, int64_t M, const int32_t* rows, const float* d_sigma,
                      const float* d_color, int64_t d_color_stride, float* d_enc,
                      int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
-                     int64_t workspace_bytes, anr_stream_t stream, float loss_scale = 0.0f,
-                     const float* tile_max = nullptr) {
+                     int64_t workspace_bytes, anr_stream_t stream, float loss_scale = 0.0f) {
   const int v = variant(pos, dir);
-  ANR_CHECK_ARG(tile_max == nullptr || (rows == nullptr && loss_scale == 0.0f),
-                "anr_ingp_field_bwd: per-tile maxima need dense rows and the dynamic scale");
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_bwd: unsupported pos/dir MLP pair");
   ANR_CHECK_ARG(loss_scale == 0.0f || (loss_scale > 0.0f && mma_dtype == ANR_F16 && rows == nullptr),
                 "anr_ingp_field_bwd: reference numerics need f16 MMA and dense rows");
@@ -1950,7 +1936,6 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   a.g_dir = g_dir;
   a.rows = rows;
   a.loss_scale = loss_scale;
-  a.tile_max = tile_max;
   const int rc = dispatch(v, mma_dtype == ANR_BF16, 2, a, static_cast<float*>(workspace),
                           workspace_bytes, reinterpret_cast<hipStream_t>(stream));
   ANR_CHECK_ARG(rc != 2,
@@ -1980,19 +1965,6 @@ extern "C" int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* d
   return field_bwd(pos, dir, mma_dtype, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
                    d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir,
                    workspace, workspace_bytes, stream);
-}
-
-extern "C" int anr_ingp_field_bwd_tm(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                     int32_t mma_dtype, const void* packed, const void* enc,
-                                     int64_t enc_stride, const float* dirs, int64_t n_per_ray,
-                                     int64_t M, const float* d_sigma, const float* d_color,
-                                     int64_t d_color_stride, const float* tile_max,
-                                     float* d_enc, int64_t d_enc_stride, float* g_pos,
-                                     float* g_dir, anr_stream_t stream) {
-  ANR_CHECK_ARG(tile_max || M == 0, "anr_ingp_field_bwd_tm: null tile_max");
-  return field_bwd(pos, dir, mma_dtype, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
-                   d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, nullptr,
-                   0, stream, 0.0f, tile_max);
 }
 
 extern "C" int anr_ingp_field_bwd_ref16(const anr_mlp_desc* pos, const anr_mlp_desc* dir,

@@ -29,9 +29,6 @@
 #ifndef HASH_FBS
 #define HASH_FBS 4  // samples per coordinate prefetch batch of the forward walker
 #endif
-#ifndef HASH_F3BS
-#define HASH_F3BS 4  // samples per gather batch of the v3 forward walker (f16 table)
-#endif
 #ifndef HASH_EXP
 #define HASH_EXP 0
 #endif
@@ -345,186 +342,6 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Forward v3 (F = 2): v1's thread mapping (one thread per (chunk, level)), walked in
-// batches of BS samples so that a wave pays ONE gather round trip per batch instead of
-// one per sample. v1 waited for the gathers of every sample on which any of its lanes
-// changed cell — on the fine levels that is nearly every sample. Here the cells of all BS
-// samples are formed first, the corner gathers of every sample that enters a new cell
-// are issued back to back (raw features, nothing computed on them), then the next
-// batch's coordinates; the interpolation resolves each sample's corners afterwards
-// (new gather or the previous sample's corners, a select). Same corner order and fma
-// chain as v1, so results are bit-identical to it.
-template <typename TT>
-struct RawF2;
-template <>
-struct RawF2<__half> {
-  using type = uint32_t;  // the two f16 features of one corner
-  __device__ static type load(const __half* p) { return *reinterpret_cast<const uint32_t*>(p); }
-  __device__ static type blend(type n, type o, uint32_t keep) { return (o & keep) | (n & ~keep); }
-  __device__ static void unpack(type r, float* v) {
-    const float2 f = __half22float2(__builtin_bit_cast(__half2, r));
-    v[0] = f.x;
-    v[1] = f.y;
-  }
-};
-template <>
-struct RawF2<float> {
-  using type = float2;
-  __device__ static type load(const float* p) { return *reinterpret_cast<const float2*>(p); }
-  __device__ static type blend(type n, type o, uint32_t keep) {
-    return float2{__uint_as_float((__float_as_uint(o.x) & keep) | (__float_as_uint(n.x) & ~keep)),
-                  __uint_as_float((__float_as_uint(o.y) & keep) | (__float_as_uint(n.y) & ~keep))};
-  }
-  __device__ static void unpack(type r, float* v) {
-    v[0] = r.x;
-    v[1] = r.y;
-  }
-};
-
-// All 2^D corner indices of a cell (LevelIdx::corner for every c), with the dense wrap as
-// one rarely-taken branch for the whole cell.
-template <int D>
-__device__ __forceinline__ void cell_corners(const LevelIdx<D>& li, const uint32_t* cell,
-                                             uint32_t* idx) {
-  uint32_t comp[D][2];
-  li.dims(cell, comp);
-  uint32_t sum[1 << D];
-  bool wrap = false;
-#pragma unroll
-  for (int c = 0; c < (1 << D); ++c) {
-    uint32_t hx = 0u, sm = 0u;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      hx ^= comp[d][(c >> d) & 1];
-      sm += comp[d][(c >> d) & 1];
-    }
-    sum[c] = sm;
-    idx[c] = li.hashed ? (hx & (li.T - 1u)) : sm;
-    wrap = wrap || (!li.hashed && sm >= li.T);
-  }
-  if (wrap) {
-#pragma unroll
-    for (int c = 0; c < (1 << D); ++c)
-      if (!li.hashed && sum[c] >= li.T) {
-        const uint32_t s1 = sum[c] - li.T;
-        idx[c] = s1 < li.T ? s1 : sum[c] % li.T;
-      }
-  }
-}
-
-template <int D, typename TT, typename TO, int BS>
-__global__ void __launch_bounds__(256) hashgrid_fwd_v3_kernel(
-    GridLevels G, int n_levels, int lpw, int n_groups, const float* __restrict__ x,
-    int64_t x_stride, int64_t M, int64_t K, const TT* __restrict__ table,
-    TO* __restrict__ out, int64_t out_stride) {
-  constexpr int NCR = 1 << D;
-  using R = RawF2<TT>;
-  using raw_t = typename R::type;
-  const int lane = static_cast<int>(threadIdx.x & 63);
-  const int lg = static_cast<int>(blockIdx.x % n_groups);
-  const int64_t wave_in = (static_cast<int64_t>(blockIdx.x / n_groups) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t chunk = wave_in * (64 / lpw) + lane / lpw;
-  const int level = lg * lpw + lane % lpw;
-  const int64_t m0 = chunk * K;
-  if (level >= n_levels || m0 >= M) return;
-  const int64_t m1 = m0 + K < M ? m0 + K : M;
-
-  const float scale = G.scale[level];
-  const TT* __restrict__ grid = table + static_cast<int64_t>(G.offset[level]) * 2;
-  LevelIdx<D> li;
-  li.init(G.size[level], G.res[level]);
-
-  uint32_t cell[D];
-  bool have = false;
-#pragma unroll
-  for (int d = 0; d < D; ++d) cell[d] = 0u;
-  raw_t cur[NCR];
-#pragma unroll
-  for (int c = 0; c < NCR; ++c) cur[c] = raw_t{};
-
-  float xa[BS][D], xb[BS][D];
-  auto load_batch = [&](int64_t mb, float (*xo)[D]) {
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      const int64_t m = mb + j < m1 ? mb + j : m1 - 1;  // clamped: no branch
-#pragma unroll
-      for (int d = 0; d < D; ++d) xo[j][d] = x[m * x_stride + d];
-    }
-  };
-  // one batch: coordinates xc (loaded one batch earlier), next batch's into xo
-  auto batch = [&](int64_t mb, float (*xc)[D], float (*xo)[D]) {
-    uint32_t g[BS][D];
-    float w[BS][D];
-    bool chg[BS];
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      bool same = j > 0 || have;
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const float p = fmaf(scale, xc[j][d], 0.5f);
-        const float fl = floorf(p);
-        g[j][d] = static_cast<uint32_t>(static_cast<int>(fl));
-        w[j][d] = p - fl;
-        same = same && (g[j][d] == (j > 0 ? g[j - 1][d] : cell[d]));
-      }
-      chg[j] = !same;
-    }
-    // gathers of every sample that enters a new cell, all in flight together
-    raw_t nv[BS][NCR];
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-#pragma unroll
-      for (int c = 0; c < NCR; ++c) nv[j][c] = raw_t{};
-      if (chg[j]) {
-        uint32_t idx[NCR];
-        cell_corners<D>(li, g[j], idx);
-#pragma unroll
-        for (int c = 0; c < NCR; ++c) nv[j][c] = R::load(grid + static_cast<int64_t>(idx[c]) * 2);
-      }
-    }
-    load_batch(mb + BS, xo);
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      // bitwise select on a mask the optimiser cannot relate to the branch above: with a
-      // plain select it merges the two into a phi at the branch join, whose register
-      // copies then wait for each sample's gathers there
-      uint32_t keep = chg[j] ? 0u : ~0u;
-      asm volatile("" : "+v"(keep));
-#pragma unroll
-      for (int c = 0; c < NCR; ++c) cur[c] = R::blend(nv[j][c], cur[c], keep);
-      float acc[2] = {0.0f, 0.0f};
-#pragma unroll
-      for (int c = 0; c < NCR; ++c) {
-        float wt = 1.0f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[j][d] : 1.0f - w[j][d];
-        float v[2];
-        R::unpack(cur[c], v);
-        acc[0] = fmaf(wt, v[0], acc[0]);
-        acc[1] = fmaf(wt, v[1], acc[1]);
-      }
-      // samples past the chunk were clamped to its last one: same cell, same weights, so
-      // they store that sample's value again (no branch around the store)
-      const int64_t m = mb + j < m1 ? mb + j : m1 - 1;
-      store_feat<TO, 2>(out + m * out_stride + level * 2, acc);
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d) cell[d] = g[BS - 1][d];
-    have = true;
-  };
-  // uniform trip count (K is the same for every chunk; a short last chunk re-walks its
-  // last sample), so the loop runs on scalar registers and the stores need no branch.
-  // Two batches per iteration with the coordinate buffers swapped: no register copies of
-  // in-flight loads at the loop edge.
-  const int64_t n_batches = (K + BS - 1) / BS;
-  load_batch(m0, xa);
-  for (int64_t it = 0; it < n_batches; it += 2) {
-    batch(m0 + it * BS, xa, xb);
-    if (it + 1 < n_batches) batch(m0 + (it + 1) * BS, xb, xa);  // uniform
-  }
-}
-
 template <typename TG>
 __device__ __forceinline__ float load_grad(const TG* p) {
   return to_f32<TG>(*p);
@@ -626,308 +443,6 @@ struct Corners {
   // lattice offset bit of corner c (0..NC-1) along dim d >= 1
   __device__ static int bit(int c, int d) { return (c >> (d - 1)) & 1; }
 };
-
-// Map the per-lane corners of the old cell onto the new cell (same x): returns, for each
-// old corner, the new corner index or -1 if it leaves the new cell.
-template <int D>
-__device__ __forceinline__ void corner_shift(const uint32_t* oldc, const uint32_t* newc,
-                                             bool same_x, int* map) {
-#pragma unroll
-  for (int c = 0; c < Corners<D>::NC; ++c) {
-    bool keep = same_x;
-    int nc = 0;
-#pragma unroll
-    for (int d = 1; d < D; ++d) {
-      const int nb = static_cast<int>(oldc[d] + Corners<D>::bit(c, d)) - static_cast<int>(newc[d]);
-      keep = keep && (nb == 0 || nb == 1);
-      nc |= (nb & 1) << (d - 1);
-    }
-    map[c] = keep ? nc : -1;
-  }
-}
-
-template <int D>
-__device__ __forceinline__ uint32_t corner_index(const uint32_t* cell, int b, int c,
-                                                 uint32_t T, uint32_t res) {
-  uint32_t gc[D];
-  gc[0] = cell[0] + b;
-#pragma unroll
-  for (int d = 1; d < D; ++d) gc[d] = cell[d] + Corners<D>::bit(c, d);
-  return grid_index<D>(T, res, gc);
-}
-
-template <int D, typename TT, typename TO>
-__global__ void __launch_bounds__(256) hashgrid_fwd_v2_kernel(
-    GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
-    int64_t K, const TT* __restrict__ table, TO* __restrict__ out, int64_t out_stride) {
-  constexpr int NC = Corners<D>::NC;
-  const int lane = threadIdx.x & 63;
-  const int level = lane >> 2, b = (lane >> 1) & 1, f = lane & 1;
-  const int64_t chunk = __builtin_amdgcn_readfirstlane(
-      static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6));
-  const int64_t m0 = chunk * K;
-  if (m0 >= M) return;  // wave-uniform
-  const int64_t m1 = m0 + K < M ? m0 + K : M;
-  const bool active = level < n_levels;
-  const int lv = active ? level : 0;
-  const float scale = G.scale[lv];
-  const uint32_t res = G.res[lv];
-  const uint32_t T = G.size[lv];
-  const TT* __restrict__ grid = table + static_cast<int64_t>(G.offset[lv]) * 2 + f;
-
-  uint32_t cell[D];
-  bool have = false;
-#pragma unroll
-  for (int d = 0; d < D; ++d) cell[d] = 0u;
-  float val[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) val[c] = 0.0f;
-
-  for (int64_t m = m0; m < m1; ++m) {
-    float w[D];
-    uint32_t g[D];
-    bool same = have;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const float p = fmaf(scale, x[m * x_stride + d], 0.5f);
-      const float fl = floorf(p);
-      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
-      w[d] = p - fl;
-      same = same && (g[d] == cell[d]);
-    }
-    if (active && !same) {
-      int map[NC];
-      corner_shift<D>(cell, g, have && g[0] == cell[0], map);
-      float nval[NC];
-      bool got[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        nval[c] = 0.0f;
-        got[c] = false;
-      }
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int c2 = 0; c2 < NC; ++c2)
-          if (map[c] == c2) {
-            nval[c2] = val[c];
-            got[c2] = true;
-          }
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        if (!got[c]) nval[c] = to_f32<TT>(grid[static_cast<int64_t>(corner_index<D>(g, b, c, T, res)) * 2]);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) val[c] = nval[c];
-#pragma unroll
-      for (int d = 0; d < D; ++d) cell[d] = g[d];
-      have = true;
-    }
-    // partial sum over this lane's corners, in tcnn's weight order (x, then y, z)
-    const float wx = b ? w[0] : 1.0f - w[0];
-    float part = 0.0f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      float wt = wx;
-#pragma unroll
-      for (int d = 1; d < D; ++d) wt *= Corners<D>::bit(c, d) ? w[d] : 1.0f - w[d];
-      part = fmaf(wt, val[c], part);
-    }
-    // add the partner lane (other x-offset): lane ^ 2 within the quad (DPP quad_perm 2,3,0,1)
-    const float other = __int_as_float(__builtin_amdgcn_update_dpp(
-        0, __float_as_int(part), 0x4E, 0xF, 0xF, false));
-    const float tot = b ? other + part : part + other;
-    if (active && b == 0) out[m * out_stride + level * 2 + f] = from_f32<TO>(tot);
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Forward v4 (F = 2): one thread per SAMPLE, looping over the levels, tiny-cuda-nn's
-// decomposition with gfx950's wave64 (64 consecutive samples of one ray per wavefront).
-// Every level's 2^D corners are gathered for every sample: on the coarse levels all
-// lanes of a wavefront read the same few lines (one L1 lookup serves them), on the fine
-// levels the gathers of the wavefront's ~17 distinct cells per level go out together.
-// Unlike the walkers (v1-v3) there is no data-dependent branch: the per-sample work is
-// one straight unrolled stream of index math, gathers and FMAs, and the compiler keeps
-// several levels' gathers in flight. Same corner order and fma chain as v1, so the
-// results are bit-identical to it.
-template <int D, typename TT, typename TO, int NL>
-__global__ void __launch_bounds__(256) hashgrid_fwd_v4_kernel(
-    GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride, int64_t M,
-    const TT* __restrict__ table, TO* __restrict__ out, int64_t out_stride) {
-  const int64_t m = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  float xv[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) xv[d] = x[m * x_stride + d];
-  TO* __restrict__ orow = out + m * out_stride;
-#pragma unroll
-  for (int level = 0; level < NL; ++level) {
-    if (level >= n_levels) continue;  // (continue, not break: keeps the loop unrollable)
-    const float scale = G.scale[level];
-    LevelIdx<D> li;
-    li.init(G.size[level], G.res[level]);
-    const TT* __restrict__ grid = table + static_cast<int64_t>(G.offset[level]) * 2;
-    float w[D];
-    uint32_t g[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const float p = fmaf(scale, xv[d], 0.5f);
-      const float fl = floorf(p);
-      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
-      w[d] = p - fl;
-    }
-    uint32_t idx[1 << D];
-    cell_corners<D>(li, g, idx);
-    typename RawF2<TT>::type raw[1 << D];
-#pragma unroll
-    for (int c = 0; c < (1 << D); ++c) raw[c] = RawF2<TT>::load(grid + static_cast<int64_t>(idx[c]) * 2);
-    float acc[2] = {0.0f, 0.0f};
-#pragma unroll
-    for (int c = 0; c < (1 << D); ++c) {
-      float wt = 1.0f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
-      float v[2];
-      RawF2<TT>::unpack(raw[c], v);
-      acc[0] = fmaf(wt, v[0], acc[0]);
-      acc[1] = fmaf(wt, v[1], acc[1]);
-    }
-    store_feat<TO, 2>(orow + level * 2, acc);
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Forward v5 (F = 2, f16 table): v1's walker (one lane per (chunk, level), corners of
-// the current cell kept in registers) with the corner gathers COMPACTED across the
-// wavefront. In v1 a wavefront of 16 levels x 4 chunks executes its 2^D gather
-// instructions on nearly every sample, because almost always some lane enters a new
-// cell, while on average only ~5 of the 64 lanes do: the texture addresser, not the
-// memory system, bounds it (TA busy 85 % of the kernel; profiles/r02_sq_bench.txt).
-// Here the lanes that enter a new cell write their 2^D corner indices to a per-wave LDS
-// list; the wave then gathers the list densely, 64 corners per instruction (usually
-// one instruction for all of them), writes the values back to the list, and each lane
-// reads its own 2^D. Same corner values and the same fma chain as v1: bit-identical.
-template <int D, typename TO>
-__global__ void __launch_bounds__(256) hashgrid_fwd_v5_kernel(
-    GridLevels G, int n_levels, int lpw, int n_groups, const float* __restrict__ x,
-    int64_t x_stride, int64_t M, int64_t K, const __half* __restrict__ table,
-    TO* __restrict__ out, int64_t out_stride) {
-  constexpr int NC = 1 << D;
-  __shared__ uint32_t list[4][64 * NC];  // per wave: corner entry index, then its value
-  const int lane = static_cast<int>(threadIdx.x & 63);
-  const int wv = static_cast<int>(threadIdx.x >> 6);
-  uint32_t* __restrict__ L = list[wv];
-  const int lg = static_cast<int>(blockIdx.x % n_groups);
-  const int64_t wave_in = (static_cast<int64_t>(blockIdx.x / n_groups) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t chunk = wave_in * (64 / lpw) + lane / lpw;
-  const int level_raw = lg * lpw + lane % lpw;
-  const int64_t m0 = chunk * K;
-  const bool lane_ok = level_raw < n_levels && m0 < M;
-  const int level = lane_ok ? level_raw : 0;  // inactive lanes still take part in the wave
-  const int64_t m1 = lane_ok ? (m0 + K < M ? m0 + K : M) : m0;
-  const uint32_t* __restrict__ tab = reinterpret_cast<const uint32_t*>(table);  // f16 pairs
-
-  const float scale = G.scale[level];
-  const uint32_t off = G.offset[level];
-  LevelIdx<D> li;
-  li.init(G.size[level], G.res[level]);
-
-  uint32_t cell[D];
-  bool have = false;
-#pragma unroll
-  for (int d = 0; d < D; ++d) cell[d] = 0u;
-  uint32_t raw[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) raw[c] = 0u;
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-
-  auto step = [&](int64_t m, const float* xv, bool act) {
-    float w[D];
-    uint32_t g[D];
-    bool same = have;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const float p = fmaf(scale, xv[d], 0.5f);
-      const float fl = floorf(p);
-      g[d] = static_cast<uint32_t>(static_cast<int>(fl));
-      w[d] = p - fl;
-      same = same && (g[d] == cell[d]);
-    }
-    const bool changed = act && !same;
-    const uint64_t mask = __ballot(changed);
-    if (mask != 0ull) {  // wave-uniform
-      const int rank = __popcll(mask & below);
-      if (changed) {
-        uint32_t idx[NC];
-        cell_corners<D>(li, g, idx);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) L[rank * NC + c] = off + idx[c];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int total = __popcll(mask) * NC;
-      for (int b = 0; b < total; b += 64) {  // usually one pass
-        const int k = b + lane;
-        if (k < total) L[k] = tab[L[k]];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (changed) {
-        have = true;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) raw[c] = L[rank * NC + c];
-#pragma unroll
-        for (int d = 0; d < D; ++d) cell[d] = g[d];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (!act) return;
-    float acc[2] = {0.0f, 0.0f};
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      float wt = 1.0f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
-      float v[2];
-      RawF2<__half>::unpack(raw[c], v);
-      acc[0] = fmaf(wt, v[0], acc[0]);
-      acc[1] = fmaf(wt, v[1], acc[1]);
-    }
-    store_feat<TO, 2>(out + m * out_stride + level * 2, acc);
-  };
-
-  // coordinates prefetched one batch ahead (indices clamped: no branch around the loads);
-  // the loop runs the wave's longest chunk (K samples) on every lane
-  constexpr int BS = HASH_FBS;
-  float xb[BS][D], xn[BS][D];
-  const int64_t mlast = m1 > m0 ? m1 - 1 : m0;
-  auto load_batch = [&](int64_t mb, float (*xo)[D]) {
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      int64_t mm = mb + j < m1 ? mb + j : mlast;
-      if (mm >= M) mm = M - 1;
-#pragma unroll
-      for (int d = 0; d < D; ++d) xo[j][d] = x[mm * x_stride + d];
-    }
-  };
-  load_batch(m0, xb);
-  for (int64_t jb = 0; jb < K; jb += BS) {
-    load_batch(m0 + jb + BS, xn);
-#pragma unroll
-    for (int j = 0; j < BS; ++j) {
-      const int64_t m = m0 + jb + j;
-      step(m, xb[j], jb + j < K && m < m1);
-    }
-#pragma unroll
-    for (int j = 0; j < BS; ++j)
-#pragma unroll
-      for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
-  }
-}
 
 // ---------------------------------------------------------------------------------------
 // Forward v6 (F = 2, L <= 16): v1's decomposition (lane = one level of one of the 4
@@ -1309,23 +824,20 @@ static int64_t pick_chunk_v2(int64_t M) {
 
 // Kernel generation per direction. Mode 0 (default): forward v6, backward v2 (measured
 // fastest on the ray-coherent bench workload; v6 falls back to v1 above 16 levels or
-// past 32-bit buffer offsets); 1: both v1; 2: both v2; 3: forward v3 (F = 2; v1
-// otherwise), backward v2; 4 / 5: forward v4 / v5, backward v2; 6: forward v1, backward
-// v2 (the previous default); 7: as 0 with the backward's run-time-stride instantiation
-// (A/B of the compile-time strides). ANR_HASHGRID_MODE or anr_hashgrid_force_v1() selects it (test
-// hook). Measured on the bench coordinates (profiles/r02_hash_fwd_v6_v7_ab.log): the
-// forward spends ~0.35 of its ~0.65 ms on the corner gathers' memory traffic (0.29 ms with
-// no gathers at all) and is not issue-bound (v6 halves the gather path's instructions
-// for 3 %; one 8-B load per x-pair instead of two 4-B loads: 4 %).
+// past 32-bit buffer offsets); 1: both v1 (the generic kernels every shape falls back
+// to); 6: forward v1, backward v2 (the r01 default); 7: as 0 with the backward's run-time-
+// stride instantiation (A/B of the compile-time strides). ANR_HASHGRID_MODE or
+// anr_hashgrid_force_v1() selects it (test hook). The r02 forward experiments v2-v5
+// (x-pair lanes, batched gathers, one thread per sample, LDS-compacted gathers) measured
+// slower than v6 and were removed in r04 (profiles/r02_hash_fwd_v6_v7_ab.log). On the
+// bench coordinates the forward spends ~0.35 of its ~0.65 ms on the corner gathers' memory
+// traffic (0.29 ms with no gathers at all) and is not issue-bound.
+static bool valid_mode(int m) { return m == 0 || m == 1 || m == 6 || m == 7; }
 static int g_hashgrid_mode = [] {
   const char* e = getenv("ANR_HASHGRID_MODE");
-  return (e && e[0] >= '0' && e[0] <= '7') ? e[0] - '0' : 0;
+  return (e && e[0] >= '0' && e[0] <= '9' && valid_mode(e[0] - '0')) ? e[0] - '0' : 0;
 }();
-static bool fwd_v2() { return g_hashgrid_mode == 2; }
-static bool fwd_v3() { return g_hashgrid_mode == 3; }
-static bool fwd_v4() { return g_hashgrid_mode == 4; }
-static bool fwd_v5() { return g_hashgrid_mode == 5; }
-static bool fwd_v6() { return g_hashgrid_mode == 0; }
+static bool fwd_v6() { return g_hashgrid_mode == 0 || g_hashgrid_mode == 7; }
 static bool bwd_v2() { return g_hashgrid_mode != 1; }
 
 // Levels per wavefront of the forward walker (1, 2, 4, 8, 16, 32 or 64).
@@ -1354,36 +866,6 @@ template <int D, int F>
 static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const float* x,
                       int64_t x_stride, int64_t M, const void* table, int32_t tdt,
                       void* out, int32_t odt, int64_t out_stride, hipStream_t s) {
-  if (F == 2 && d->n_levels <= 16 && fwd_v2()) {
-    const int64_t K = pick_chunk_v2(M);
-    const int64_t waves = ceil_div(M, K);
-    const dim3 grid(static_cast<unsigned>(ceil_div(waves, 4))), block(256);
-#define ANR_HG_FWD2(TT, TO)                                                                  \
-  hipLaunchKernelGGL((hashgrid_fwd_v2_kernel<D, TT, TO>), grid, block, 0, s, G, d->n_levels, \
-                     x, x_stride, M, K, static_cast<const TT*>(table), static_cast<TO*>(out), \
-                     out_stride)
-    if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD2(__half, __half);
-    else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD2(__half, float);
-    else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD2(float, __half);
-    else ANR_HG_FWD2(float, float);
-#undef ANR_HG_FWD2
-    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v2)");
-    return ANR_OK;
-  }
-  if (F == 2 && d->n_levels <= 16 && fwd_v4()) {
-    const dim3 grid(static_cast<unsigned>(ceil_div(M, 256))), block(256);
-#define ANR_HG_FWD4(TT, TO)                                                                  \
-  hipLaunchKernelGGL((hashgrid_fwd_v4_kernel<D, TT, TO, 16>), grid, block, 0, s, G,          \
-                     d->n_levels, x, x_stride, M, static_cast<const TT*>(table),             \
-                     static_cast<TO*>(out), out_stride)
-    if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD4(__half, __half);
-    else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD4(__half, float);
-    else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD4(float, __half);
-    else ANR_HG_FWD4(float, float);
-#undef ANR_HG_FWD4
-    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v4)");
-    return ANR_OK;
-  }
   if (F == 2 && d->n_levels <= 16 && fwd_v6()) {
     // 32-bit buffer offsets: every byte range must stay below 2^31
     const int64_t esz_t = tdt == ANR_F16 ? 2 : 4, esz_o = odt == ANR_F16 ? 2 : 4;
@@ -1417,31 +899,6 @@ static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
   const int64_t chunks = ceil_div(M, K);
   const int64_t blocks_per_group = ceil_div(ceil_div(chunks, 64 / lpw), 4);
   const dim3 grid(static_cast<unsigned>(blocks_per_group * n_groups)), block(256);
-  if (F == 2 && fwd_v5() && tdt == ANR_F16) {
-    if (odt == ANR_F16)
-      hipLaunchKernelGGL((hashgrid_fwd_v5_kernel<D, __half>), grid, block, 0, s, G, d->n_levels,
-                         lpw, n_groups, x, x_stride, M, K, static_cast<const __half*>(table),
-                         static_cast<__half*>(out), out_stride);
-    else
-      hipLaunchKernelGGL((hashgrid_fwd_v5_kernel<D, float>), grid, block, 0, s, G, d->n_levels,
-                         lpw, n_groups, x, x_stride, M, K, static_cast<const __half*>(table),
-                         static_cast<float*>(out), out_stride);
-    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v5)");
-    return ANR_OK;
-  }
-  if (F == 2 && fwd_v3()) {
-#define ANR_HG_FWD3(TT, TO, BS)                                                             \
-  hipLaunchKernelGGL((hashgrid_fwd_v3_kernel<D, TT, TO, BS>), grid, block, 0, s, G,         \
-                     d->n_levels, lpw, n_groups, x, x_stride, M, K,                          \
-                     static_cast<const TT*>(table), static_cast<TO*>(out), out_stride)
-    if (tdt == ANR_F16 && odt == ANR_F16) ANR_HG_FWD3(__half, __half, HASH_F3BS);
-    else if (tdt == ANR_F16 && odt == ANR_F32) ANR_HG_FWD3(__half, float, HASH_F3BS);
-    else if (tdt == ANR_F32 && odt == ANR_F16) ANR_HG_FWD3(float, __half, 4);
-    else ANR_HG_FWD3(float, float, 4);
-#undef ANR_HG_FWD3
-    ANR_CHECK_LAUNCH("anr_hashgrid_fwd(v3)");
-    return ANR_OK;
-  }
 #define ANR_HG_FWD(TT, TO)                                                                  \
   hipLaunchKernelGGL((hashgrid_fwd_kernel<D, F, TT, TO>), grid, block, 0, s, G,             \
                      d->n_levels, lpw, n_groups, x, x_stride, M, K,                          \
@@ -1500,8 +957,10 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 }  // namespace anr
 
 extern "C" int anr_hashgrid_force_v1(int32_t mode) {
+  ANR_CHECK_ARG(anr::valid_mode(mode), "anr_hashgrid_force_v1: mode %d is not 0, 1, 6 or 7",
+                mode);
   const int prev = anr::g_hashgrid_mode;
-  anr::g_hashgrid_mode = (mode >= 0 && mode <= 7) ? mode : 0;
+  anr::g_hashgrid_mode = mode;
   return prev;
 }
 

@@ -144,12 +144,11 @@ int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x, int64_t x_strid
                      int64_t M, const void* table, int32_t table_dtype, void* out,
                      int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
 
-/* Kernel generation (test / A-B hook; process-wide; returns the previous mode; also
- * ANR_HASHGRID_MODE): 0 = default (forward v6 branch-free walker -- v1 above 16 levels or
- * past 32-bit buffer offsets -- backward v2 four-lanes-per-level), 1 = v1 both,
- * 2 = v2 both, 3 = forward v3 (batched gathers, F = 2) + backward v2, 4 / 5 = forward v4
- * (per sample) / v5 (LDS-compacted gathers) + backward v2, 6 = forward v1 + backward v2
- * (the r01 default), 7 = mode 0 with the backward's run-time-stride instantiation. */
+/* Kernel generation (test / A-B hook; process-wide; returns the previous mode, or
+ * ANR_E_INVALID for an unknown mode; also ANR_HASHGRID_MODE): 0 = default (forward v6
+ * branch-free walker -- v1 above 16 levels or past 32-bit buffer offsets -- backward v2
+ * four-lanes-per-level), 1 = v1 both, 6 = forward v1 + backward v2 (the r01 default),
+ * 7 = mode 0 with the backward's run-time-stride instantiation. */
 int anr_hashgrid_force_v1(int32_t mode);
 
 /* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)
@@ -295,17 +294,6 @@ int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t
                        const float* d_color, int64_t d_color_stride, float* d_enc,
                        int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
                        int64_t workspace_bytes, anr_stream_t stream);
-/* anr_ingp_field_bwd with the f16 gradient scale's input supplied: tile_max[t] (f32,
- * ceil(M/32) entries) = max over rows [32t, 32t+32) of |d_color[r][0..n_output)| and
- * |d_sigma[r]|, as anr_composite_bwd_tm writes it while producing d_color / d_sigma. No
- * separate max-reduction pass over them and no workspace; results bit-identical to
- * anr_ingp_field_bwd. Dense rows only. */
-int anr_ingp_field_bwd_tm(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,
-                          const void* packed, const void* enc, int64_t enc_stride,
-                          const float* dirs, int64_t n_per_ray, int64_t M,
-                          const float* d_sigma, const float* d_color, int64_t d_color_stride,
-                          const float* tile_max, float* d_enc, int64_t d_enc_stride,
-                          float* g_pos, float* g_dir, anr_stream_t stream);
 
 /* The same kernels over occupancy-compacted samples (anr_occupancy_compact): row r of
  * enc / d_enc is dense sample rows[r] (int32, ray-major index < n_rays * n_per_ray) of
@@ -415,19 +403,6 @@ int anr_composite_bwd(const float* z, float z_scale, const void* color, const vo
                       const void* d_surf, const void* d_weights, const void* d_alpha,
                       void* d_color, void* d_sigma, void* d_color_surf, float* d_z,
                       anr_stream_t stream);
-/* anr_composite_bwd that also writes tile_max[t] = max over rows [32t, 32t+32) of the B*N
- * ray-major rows of |d_color[r][c]| (all C) and |d_sigma[r]|: the input of the fused
- * field backward's f16 gradient scale (anr_ingp_field_bwd_tm). d_color and d_sigma are
- * required; supported when anr_composite_tile_max_supported() says so. */
-int anr_composite_bwd_tm(const float* z, float z_scale, const void* color, const void* sigma,
-                         const void* color_surf, int32_t io_dtype, int64_t B, int32_t N,
-                         int32_t C, int32_t S, const void* d_color_map, const void* d_atmo,
-                         const void* d_surf, const void* d_weights, const void* d_alpha,
-                         void* d_color, void* d_sigma, void* d_color_surf, float* d_z,
-                         float* tile_max, anr_stream_t stream);
-/* 1 when anr_composite_bwd_tm serves this shape (f32 io, C = 4, S = 1, N a multiple of 32
- * on the register-blocked kernels), else 0. */
-int anr_composite_tile_max_supported(int32_t io_dtype, int32_t N, int32_t C, int32_t S);
 
 /* ------------------------------------------------------------------------------------
  * K9: losses (losses.py:5-33) on pred = take_along_dim(color_map, irgb_idx)

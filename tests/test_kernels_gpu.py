@@ -134,14 +134,13 @@ def _grid_inputs(dev, cfg, M, coherent, seed=0):
 
 
 # hash-grid kernel generations (anr_hashgrid_force_v1 modes): "default" = forward v6
-# (branch-free corners, buffer addressing) with backward v2, "v2" = both v2, "v1" = both v1,
-# "v3" = forward v3 (batched gathers) with backward v2, "v4" = forward v4 (one thread per
-# sample) with backward v2, "v5" = forward v5 (compacted gathers), "v1fwd" = forward v1
-# walker with backward v2 (the r01 default)
-_HASH_MODES = {"default": 0, "v2": 2, "v1": 1, "v3": 3, "v4": 4, "v5": 5, "v1fwd": 6}
+# (branch-free corners, buffer addressing) with backward v2, "v1" = both v1 (the generic
+# kernels), "v1fwd" = forward v1 walker with backward v2 (the r01 default), "rtstride" =
+# the default with the backward's run-time-stride instantiation
+_HASH_MODES = {"default": 0, "v1": 1, "v1fwd": 6, "rtstride": 7}
 
 
-@pytest.fixture(params=["default", "v2", "v1", "v3", "v4", "v5", "v1fwd"])
+@pytest.fixture(params=["default", "v1", "v1fwd", "rtstride"])
 def hash_path(request):
     from atmonr_amd import _lib
 
@@ -1056,10 +1055,9 @@ def test_ingp_field_bench_size(dev, mma):
 
 
 @pytest.mark.parametrize("tdt", ["f16", "f32"])
-def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
-    """The per-sample forward (v4), the compacted-gather walker (v5, f16 tables), the
-    buffer-addressed walker (v6) and the walker (v1) evaluate the same corner order and fma
-    chain: identical outputs, f16 and f32 tables, at a bench-like shape."""
+def test_hashgrid_fwd_v6_bit_identical_to_v1(dev, tdt):
+    """The buffer-addressed walker (v6) and the walker (v1) evaluate the same corner order
+    and fma chain: identical outputs, f16 and f32 tables, at a bench-like shape."""
     from atmonr_amd import _lib
 
     d = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, 19)
@@ -1069,8 +1067,7 @@ def test_hashgrid_fwd_v4_bit_identical_to_v1(dev, tdt):
     table = ((torch.rand(d.n_params, device=dev, generator=gen) * 2 - 1) * 1e-2).to(dt)
     outs = []
     lib = _lib.load()
-    modes = (1, 4, 5, 0) if tdt == "f16" else (1, 4, 0)  # v5: f16 tables; 0: v6
-    for mode in modes:
+    for mode in (1, 0):  # v1, v6
         prev = lib.anr_hashgrid_force_v1(mode)
         out = torch.empty(x.shape[0], 32, device=dev, dtype=dt)
         _lib.call("anr_hashgrid_fwd", ctypes.byref(d), x.data_ptr(), 3, x.shape[0],

@@ -805,10 +805,14 @@ static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
   return true;
 }
 
-// v2: one chunk per wave; aim for >= 32K waves (8 per SIMD on 1024 SIMDs, x4 slack) with
-// chunks of up to 256 samples: every chunk ends with a flush of all its corners, and at
-// the bench size (8.39 M samples, 32K waves) 256 beat 128 / 192 / 384 (hash bwd 1.27 ->
-// 1.17 ms in the timed region; profiles/r01_hash_bwd_chunk_sweep.log).
+// v2: one chunk per wave. Every chunk ends with a flush of all its held corners, so a
+// chunk should be long (requests per sample on the bench coordinates, tools/
+// hash_bwd_requests.py: K = 32 / 64 / 128 / 256 / 512 -> 4.42 / 3.33 / 2.79 / 2.51 / 2.37),
+// but the grid still needs waves to hide the walk's latency. Measured (r04 sweep,
+// profiles/r04_hash_bwd_ksweep.md): at 1,024 rays x 1,024 samples K = 256 (4,096 waves)
+// takes 0.176 ms against 0.295 ms at the r03 rule's K = 32 and 0.244 ms at K = 512; at
+// 8,192 rays K = 256 / 512 / 1024 take 1.219 / 1.200 / 1.287 ms. Rule: 256 samples per
+// chunk down to 4,096 chunks, shorter below that.
 static int64_t env_k(const char* name) {
   const char* e = getenv(name);  // profiling override of the chunk length
   return e ? atoll(e) : 0;
@@ -816,7 +820,7 @@ static int64_t env_k(const char* name) {
 static int64_t pick_chunk_v2(int64_t M) {
   static const int64_t over = env_k("ANR_HASH_KB");
   if (over > 0) return over;
-  int64_t K = M / 32768;
+  int64_t K = M / 4096;
   if (K < 1) K = 1;
   if (K > 256) K = 256;
   return K;

@@ -525,30 +525,22 @@ class IngpJob:
         return out
 
     def time_dominant(self, name: str, n: int):
-        """Live duration of kernel ``name`` in graph replays: a second capture of the step
-        with timing events recorded as graph nodes around that kernel, replayed ``n``
-        times; each replay's pair is read after it completes. None if the runtime cannot
-        time events recorded inside a graph."""
+        """Duration of kernel ``name`` for a graphed job: HIP events around its launches in
+        ``n`` eager steps of the same shape right after the timed replays (the graph runs
+        the same kernels with the same arguments; ROCm's torch refuses the external events
+        that would time a node inside a replay)."""
         from atmonr_amd import _lib
 
-        g = self._graph(self.batch_size)
-        timer = _lib.KernelTimer(only={name}, external=True)
-        try:
-            g.capture(self.next_idx(), timer=timer)
-            ts = []
+        timer = _lib.KernelTimer(only={name})
+        with timer:
             for _ in range(n):
-                g(self.next_idx())
-                torch.cuda.synchronize()
-                ts += [a.elapsed_time(b) for a, b in timer.events.get(name, [])]
-        except (RuntimeError, _lib.ANRError) as e:  # noqa: BLE001
-            return {"error": str(e)[:200]}
-        finally:
-            del g
-        if not ts:
-            return None
-        return {"launches": len(ts), "total_ms": sum(ts), "avg_ms": sum(ts) / len(ts),
-                "source": "HIP events recorded inside the step's hipGraph around this kernel, "
-                          "read after each of the replays following the timed region"}
+                self.eager_step()
+        torch.cuda.synchronize()
+        st = timer.summary().get(name)
+        if st:
+            st = dict(st, source=f"HIP events around the kernel in {n} eager steps of the "
+                                 "graphed shape after the timed graph replays")
+        return st
 
     def release(self) -> None:
         self.gstep = None
@@ -854,6 +846,8 @@ def main():
                         "bytes_per_unit": mdl["bytes"] / M,
                         "fractions": {x: k[x] for x in ("hbm_frac", "mfma_frac", "atomic_frac",
                                                         "survey_model_frac") if x in k}}
+            if st.get("source"):
+                roofline["timing_source"] = st["source"]
             if "atomic_requests" in mdl:
                 roofline["atomic_requests_per_launch"] = mdl["atomic_requests"]
                 roofline["atomic_requests_per_sample"] = round(mdl["atomic_requests"] / M, 4)

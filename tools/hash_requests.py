@@ -32,7 +32,7 @@ def bwd_chunk(M: int) -> int:
     over = int(os.environ.get("ANR_HASH_KB", "0") or 0)
     if over > 0:
         return over
-    return max(1, min(256, M // 32768))
+    return max(1, min(256, M // 4096))
 
 
 def level_geometry(desc) -> list[dict]:

@@ -177,11 +177,13 @@ class FlatGradBucket:
 class ShardSegment:
     """The part of one parameter inside this rank's shard: views into the flat buffers
     (``param``, ``grad``, ``exp_avg``, ``exp_avg_sq``, ``shadow`` f16 or None) and its
-    group's ``lr`` / ``weight_decay``."""
+    group's ``lr`` / ``weight_decay`` (refreshed from the live param group every step)."""
 
-    __slots__ = ("param", "grad", "exp_avg", "exp_avg_sq", "shadow", "lr", "weight_decay")
+    __slots__ = ("param", "grad", "exp_avg", "exp_avg_sq", "shadow", "lr", "weight_decay",
+                 "group")
 
     def __init__(self, **kw):
+        self.group = None
         for k, v in kw.items():
             setattr(self, k, v)
 
@@ -204,7 +206,7 @@ def hip_adam_update(segments, step: int, betas, eps: float, decoupled: bool) -> 
               float(betas[1]), float(eps), int(decoupled), 0, _lib.stream(dev), tag="adam")
 
 
-class ShardedAdam:
+class ShardedAdam(torch.optim.Optimizer):
     """Optimizer sharded over the data-parallel ranks (ZeRO stage 1), the alternative to
     FlatGradBucket.all_reduce + a replicated FusedAdam:
 
@@ -214,9 +216,17 @@ class ShardedAdam:
        weight decay of its param group, as the replicated optimizer);
     3. ``all_gather`` of the updated slice: ``gather="f16"`` gathers the f16 compute copy
        the forward kernels read (half the bytes of f32; the f32 masters outside the slice
-       are then stale until :meth:`consolidate`, which checkpoints call), ``gather="f32"``
-       gathers the f32 parameters (every replica stays complete; the f16 copies refresh
-       from them on the next forward).
+       are then stale until :meth:`consolidate`, which :meth:`state_dict` calls),
+       ``gather="f32"`` gathers the f32 parameters (every replica stays complete; the f16
+       copies refresh from them on the next forward).
+
+    A torch Optimizer over the given param groups: ``param_groups`` stay live, so a
+    scheduler writing ``group["lr"]`` (trainer.py:113-120's ExponentialLR) reaches the
+    next step; ``state_dict()`` / ``load_state_dict()`` use torch.optim.AdamW's format
+    (per-parameter ``step`` / ``exp_avg`` / ``exp_avg_sq``, the moments all-gathered), so
+    checkpoints interchange with FusedAdam's and torch's at any rank count. A group
+    without ``weight_decay`` gets FusedAdam's default (AdamW's 1e-2 when decoupled, Adam's
+    0 otherwise).
 
     Bytes per step: reduce-scatter 4n + all-gather 2n (f16) against the all-reduce's 8n
     (a ring all-reduce is a reduce-scatter plus an all-gather of f32), and the AdamW pass
@@ -226,9 +236,13 @@ class ShardedAdam:
 
     def __init__(self, bucket: FlatGradBucket, param_groups: list, betas=(0.9, 0.999),
                  eps: float = 1e-8, decoupled: bool = True, gather: str = "f16", group=None,
-                 update=hip_adam_update):
+                 update=hip_adam_update, lr: float = 1e-3, weight_decay: float | None = None):
         if gather not in ("f16", "f32"):
             raise ValueError("gather: 'f16' or 'f32'")
+        if weight_decay is None:  # FusedAdam's default: torch.optim.AdamW's 1e-2, Adam's 0
+            weight_decay = 1e-2 if decoupled else 0.0
+        super().__init__(param_groups, dict(lr=lr, betas=tuple(betas), eps=eps,
+                                            weight_decay=weight_decay))
         self.bucket, self.group, self.gather = bucket, group, gather
         self.betas, self.eps, self.decoupled = tuple(betas), float(eps), decoupled
         self.update = update
@@ -240,17 +254,14 @@ class ShardedAdam:
                              "(FlatGradBucket(..., pad_to=world_size))")
         self.S = n_pad // self.world
         dev = bucket.flat.device
-        hp = {}
-        for g in param_groups:
-            for p in g["params"]:
-                hp[id(p)] = (float(g.get("lr", 1e-3)), float(g.get("weight_decay", 0.0)))
+        owner = {id(p): g for g in self.param_groups for p in g["params"]}
         # flat f32 parameters: every parameter becomes a view into it
         self.flat_param = torch.zeros(n_pad, device=dev, dtype=torch.float32)
         off = 0
         self._spans = []  # (param, offset)
         with torch.no_grad():
             for p in bucket.params:
-                if id(p) not in hp:
+                if id(p) not in owner:
                     raise ValueError("every bucketed parameter must be in a param group")
                 n = p.numel()
                 self.flat_param[off:off + n].copy_(p.detach().reshape(-1))
@@ -273,19 +284,23 @@ class ShardedAdam:
             a, b = max(o, lo), min(o + p.numel(), hi)
             if a >= b:
                 continue
-            lr, wd = hp[id(p)]
+            g = owner[id(p)]
             self.segments.append(ShardSegment(
                 param=self.flat_param[a:b], grad=self.grad_shard[a - lo:b - lo],
                 exp_avg=self.exp_avg[a - lo:b - lo], exp_avg_sq=self.exp_avg_sq[a - lo:b - lo],
                 shadow=None if self.shadow_shard is None else self.shadow_shard[a - lo:b - lo],
-                lr=lr, weight_decay=wd))
+                lr=float(g["lr"]), weight_decay=float(g["weight_decay"]), group=g))
         self.steps = 0
         self.masters_current = True
 
     @torch.no_grad()
-    def step(self) -> None:
+    def step(self, closure=None):
         """Reduce-scatter, update this rank's slice, all-gather (call after backward, in
         place of bucket.all_reduce() + optimizer.step())."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
         lo = self.rank * self.S
         if self.world > 1:
             dist.reduce_scatter_tensor(self.grad_shard, self.bucket.flat, op=dist.ReduceOp.AVG,
@@ -293,6 +308,9 @@ class ShardedAdam:
         else:
             self.grad_shard.copy_(self.bucket.flat[lo:lo + self.S])
         self.steps += 1
+        for sg in self.segments:  # the live group's hyper-parameters (schedulers write them)
+            sg.lr = float(sg.group["lr"])
+            sg.weight_decay = float(sg.group["weight_decay"])
         self.update(self.segments, self.steps, self.betas, self.eps, self.decoupled)
         mine = self.flat_param[lo:lo + self.S]
         if self.gather == "f16":
@@ -311,6 +329,11 @@ class ShardedAdam:
                 if hasattr(p, "_anr_shadow_ver"):
                     p._anr_shadow_ver = None  # refresh the f16 copy from the gathered f32
         self.bucket._known_zero = False
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        """The gradients are views into the bucket: zero it (never set to None)."""
+        self.bucket.zero()
 
     @torch.no_grad()
     def consolidate(self) -> None:
@@ -326,6 +349,63 @@ class ShardedAdam:
             p._anr_master_stale = False
             if hasattr(p, "_anr_shadow_ver"):
                 p._anr_shadow_ver = p._version
+
+    def _gathered(self, shard: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return shard.clone()
+        full = torch.empty(self.S * self.world, device=shard.device, dtype=shard.dtype)
+        dist.all_gather_into_tensor(full, shard.contiguous(), group=self.group)
+        return full
+
+    def state_dict(self) -> dict:
+        """torch.optim.AdamW's layout for every parameter (a collective: call on every
+        rank). Consolidates the f32 masters first."""
+        self.consolidate()
+        m, v = self._gathered(self.exp_avg), self._gathered(self.exp_avg_sq)
+        span = {id(p): o for p, o in self._spans}
+        index, groups, state = {}, [], {}
+        for g in self.param_groups:
+            ids = []
+            for p in g["params"]:
+                k = index.setdefault(id(p), len(index))
+                ids.append(k)
+                o, n = span[id(p)], p.numel()
+                state[k] = {"step": torch.tensor(float(self.steps)),
+                            "exp_avg": m[o:o + n].view_as(p).clone(),
+                            "exp_avg_sq": v[o:o + n].view_as(p).clone()}
+            groups.append({**{k: v for k, v in g.items() if k != "params"}, "params": ids})
+        return {"state": state, "param_groups": groups}
+
+    @torch.no_grad()
+    def load_state_dict(self, state_dict: dict) -> None:
+        """Load a torch.optim.AdamW / FusedAdam / ShardedAdam state dict (same parameter
+        order): this rank keeps its slice of the moments; group hyper-parameters are
+        copied into the live groups."""
+        groups = state_dict["param_groups"]
+        if len(groups) != len(self.param_groups):
+            raise ValueError("state dict has a different number of param groups")
+        span = {id(p): o for p, o in self._spans}
+        lo = self.rank * self.S
+        steps = set()
+        for g, sg in zip(self.param_groups, groups):
+            if len(g["params"]) != len(sg["params"]):
+                raise ValueError("param group sizes differ from the state dict's")
+            for k, v in sg.items():
+                if k != "params":
+                    g[k] = v
+            for p, key in zip(g["params"], sg["params"]):
+                st = state_dict["state"].get(key)
+                if not st:
+                    continue
+                steps.add(int(float(st["step"])))
+                o, n = span[id(p)], p.numel()
+                a, b = max(o, lo), min(o + n, lo + self.S)
+                if a < b:
+                    self.exp_avg[a - lo:b - lo].copy_(st["exp_avg"].reshape(-1)[a - o:b - o])
+                    self.exp_avg_sq[a - lo:b - lo].copy_(st["exp_avg_sq"].reshape(-1)[a - o:b - o])
+        if len(steps) > 1:
+            raise ValueError("ShardedAdam keeps one step count: parameters at different steps")
+        self.steps = steps.pop() if steps else 0
 
     def state_numel(self) -> int:
         return 2 * self.S

@@ -1228,10 +1228,14 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
   // 4 wavefronts x two alternating regions (consecutive layers' transposes may overlap)
   __shared__ __attribute__((aligned(16))) _Float16 trs[LT ? 4 * 2 * kLtRegion * kLtSlot : 8];
+  // the block's dW partials (pos parameters, then dir), summed here before the one global
+  // flush per block
+  __shared__ float red[N::NPOS + N::NDIR];
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
   for (int e = threadIdx.x * 8; e < N::n_packed; e += blockDim.x * 8)
     *reinterpret_cast<h8*>(wsm + e) = *reinterpret_cast<const h8*>(a.packed + e);
+  for (int e = threadIdx.x; e < N::NPOS + N::NDIR; e += blockDim.x) red[e] = 0.0f;
   __syncthreads();
   // per-tile opaque copy of the fragment base: the weight fragments are re-read from LDS
   // each tile instead of being hoisted into registers
@@ -1570,6 +1574,12 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   agpr_pin(dD0);
   agpr_pin(dP1);
   agpr_pin(dP0);
+  // dW flush: each wavefront's partials (unscaled by its own gradient scale) go into the
+  // block's LDS sums, then the block adds them to the f32 gradients with one coalesced
+  // atomic per parameter: a quarter of the r03 memory-side requests (one set per
+  // wavefront; ~33 us per launch at 1,024 wavefronts, fixed in M)
+  float* const rpos = red;
+  float* const rdir = red + N::NPOS;
   auto flush = [&](float* dst, int ld, const f4& d, int n0, int k) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1577,22 +1587,27 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   };
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
-    flush(a.g_dir + N::D2, W, dD2[kt], 0, 16 * kt + li);
-    flush(a.g_pos + N::P1, W, dP1[kt], 0, 16 * kt + li);
+    flush(rdir + N::D2, W, dD2[kt], 0, 16 * kt + li);
+    flush(rpos + N::P1, W, dP1[kt], 0, 16 * kt + li);
   }
   if constexpr (NHD == 2) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int kt = 0; kt < NT; ++kt) flush(a.g_dir + N::D1, W, dD1[nt * NT + kt], 16 * nt, 16 * kt + li);
+      for (int kt = 0; kt < NT; ++kt) flush(rdir + N::D1, W, dD1[nt * NT + kt], 16 * nt, 16 * kt + li);
   }
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
-      flush(a.g_dir + N::D0, 32, dD0[nt * 2 + kt], 16 * nt, dir_col(16 * kt + li));
-      flush(a.g_pos + N::P0, 32, dP0[nt * 2 + kt], 16 * nt, 16 * kt + li);
+      flush(rdir + N::D0, 32, dD0[nt * 2 + kt], 16 * nt, dir_col(16 * kt + li));
+      flush(rpos + N::P0, 32, dP0[nt * 2 + kt], 16 * nt, 16 * kt + li);
     }
+  __syncthreads();
+  for (int e = threadIdx.x; e < N::NPOS + N::NDIR; e += blockDim.x) {
+    const float v = red[e];
+    if (v != 0.0f) atomicAdd(e < N::NPOS ? a.g_pos + e : a.g_dir + (e - N::NPOS), v);
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1706,7 +1721,8 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
   }
   const int mode = g_bwd_mode;
   const size_t lds = (static_cast<size_t>(N::n_packed) + (mode == 0 ? waves * N::wave_lds : 0) +
-                      (mode == 2 ? 4 * 2 * kLtRegion * kLtSlot : 0)) * 2;
+                      (mode == 2 ? 4 * 2 * kLtRegion * kLtSlot : 0)) * 2 +
+                     (mode != 0 ? sizeof(float) * (N::NPOS + N::NDIR) : 0);
   if (lds > 160 * 1024) return 1;
   const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast, mode);
   if (!BF && (ws == nullptr || ws_bytes < static_cast<int64_t>(sizeof(float)) * gm.nw))

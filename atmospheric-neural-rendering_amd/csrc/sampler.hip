@@ -87,6 +87,10 @@ __device__ __forceinline__ void preprocess_point(const PrepDev& P, T px, T py, T
     const double rl = sqrt(X * X + Y * Y);
     const double sl = Y / rl;
     const double Nr = kA / sqrt(1.0 - kE * (sl * sl));
+    // x / (cos(lat) cos(lon)) (wgs_84.py:96) with cos(lon) = x / D and cos(lat) = X / rl.
+    // Deliberate deviation at x = 0 (lon = +-90 deg): the reference divides 0 by cos(lon)
+    // ~ 6e-17 (a finite value that depends on atan2's last ulp, or inf / NaN), this form
+    // stays finite; no HARP2 scene here reaches it (scenes centred on lon = +-90 deg would)
     const double alt = (D * rl) / X - Nr;
     constexpr double kDeg = 180.0 / kPi;
     double lat_d = lat * kDeg;

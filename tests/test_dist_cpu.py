@@ -331,3 +331,86 @@ def test_sharded_adam_matches_all_reduce_path(world, gather):
             assert torch.equal(a, c)  # the replicated path: identical on every rank
             assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (r, (a - b).abs().max())
         assert state == 2 * (-(-n // world))
+
+
+def _sharded_sched_worker(rank, world, port, out):
+    import sys
+
+    from tests.conftest import PKG
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from torch.optim.lr_scheduler import ExponentialLR
+
+    from atmonr_amd.parallel import FlatGradBucket, ShardedAdam
+
+    sizes = [37, 5, 1000, 3, 129]
+
+    def make():
+        g = torch.Generator().manual_seed(1)
+        return [torch.nn.Parameter(torch.randn(n, generator=g) * 0.1) for n in sizes]
+
+    def build(ps):
+        b = FlatGradBucket(ps, device=torch.device("cpu"), pad_to=world)
+        # the second group leaves weight_decay to the optimizer's default (AdamW's 1e-2)
+        opt = ShardedAdam(b, [{"params": ps[:2], "weight_decay": 0.0, "lr": 1e-2},
+                              {"params": ps[2:], "lr": 3e-3}], betas=(0.9, 0.99), eps=1e-15,
+                          gather="f32", update=_reference_adamw)
+        return b, opt
+
+    def step(ps, b, opt, k):
+        x = torch.randn(16, sum(sizes), generator=torch.Generator().manual_seed(100 * k + rank))
+        b.zero()
+        w = torch.cat([t.reshape(-1) for t in ps])
+        (((x * w).sum(1) ** 2).mean() + (w ** 3).sum()).backward()
+        opt.step()
+
+    # (a) ShardedAdam under ExponentialLR (trainer.py:113-120), 5 steps straight through
+    pa = make()
+    ba, oa = build(pa)
+    assert oa.param_groups[1]["weight_decay"] == 1e-2
+    sa = ExponentialLR(oa, gamma=0.5)
+    for k in range(5):
+        step(pa, ba, oa, k)
+        sa.step()
+    # (b) 3 steps, checkpoint (torch AdamW layout), a fresh optimizer loads it, 2 more
+    pb = make()
+    bb, ob = build(pb)
+    sb = ExponentialLR(ob, gamma=0.5)
+    for k in range(3):
+        step(pb, bb, ob, k)
+        sb.step()
+    sd = ob.state_dict()
+    assert set(sd["state"][2]) == {"step", "exp_avg", "exp_avg_sq"}
+    assert sd["state"][2]["exp_avg"].shape == (1000,) and float(sd["state"][0]["step"]) == 3
+    pc = [torch.nn.Parameter(p.detach().clone()) for p in pb]
+    bc, oc = build(pc)
+    oc.load_state_dict(sd)
+    assert oc.param_groups[1]["lr"] == 3e-3 * 0.125 and oc.steps == 3
+    for k in range(3, 5):
+        step(pc, bc, oc, k)
+        for g in oc.param_groups:
+            g["lr"] *= 0.5
+    # a torch.optim.AdamW loads the same checkpoint
+    t = torch.optim.AdamW([{"params": make()[:2]}, {"params": make()[2:]}])
+    t.load_state_dict(sd)
+    out[rank] = ([p.detach().clone() for p in pa], [p.detach().clone() for p in pc],
+                 [g["lr"] for g in oa.param_groups])
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_adam_scheduler_and_checkpoint():
+    """ShardedAdam is a torch Optimizer with live param groups: ExponentialLR's lr reaches
+    its updates; state_dict() (torch AdamW layout, moments all-gathered) loaded into a
+    fresh ShardedAdam continues bit-identically to an uninterrupted run, and loads into
+    torch.optim.AdamW (gloo, world size 2)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sharded_sched_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        pa, pc, lrs = out[r]
+        assert lrs == [1e-2 * 0.5 ** 5, 3e-3 * 0.5 ** 5]
+        for a, c in zip(pa, pc):
+            assert torch.equal(a, c)

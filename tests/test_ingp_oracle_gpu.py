@@ -51,14 +51,18 @@ pytestmark = pytest.mark.gpu
 
 IMG, BATCH, N, KS = 16, 256, 64, [0, 8]   # 8 views x 16 x 16 = 2,048 rays = 8 batches
 OPT = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
-TOL = {"f32": {"out": 1e-4, "loss": 1e-5, "grad": 2e-3},
-       "f16": {"out": 2e-2, "loss": 5e-3, "grad": 1e-1},
+# about 3x the largest error measured on MI355X (profiles/r03_ingp_oracle_records.json:
+# f32 out 2e-6 / grad 5e-6 apart from the dir MLP's f32-composite noise, which the 4x
+# oracle-noise floor below covers; f16 out 3.3e-4 / loss 8e-6 / grad 7.4e-3 (hash table);
+# bf16 grad 2.1e-3; reference numerics out / loss bit-exact, grad 8.2e-5)
+TOL = {"f32": {"out": 1e-5, "loss": 1e-6, "grad": 3e-5},
+       "f16": {"out": 1e-3, "loss": 3e-5, "grad": 2.5e-2},
        # bf16 field MLPs (8 significant bits, unscaled bf16 gradient tiles) over f16 tables
-       "bf16": {"out": 4e-2, "loss": 1e-2, "grad": 2e-1},
+       "bf16": {"out": 1e-3, "loss": 3e-5, "grad": 1e-2},
        # reference numerics vs reference semantics: the composite / loss are bit-exact
        # restatements (test_ref16_gpu.py); what differs is the f16 MLPs' accumulation
        # order (MFMA f32 vs the oracle's f64 then f16) and the hash gradient's summation
-       "ref16": {"out": 1e-2, "loss": 5e-3, "grad": 1e-3}}
+       "ref16": {"out": 1e-5, "loss": 1e-5, "grad": 3e-4}}
 _REC = {}
 
 

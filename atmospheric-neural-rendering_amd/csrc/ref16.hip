@@ -79,9 +79,15 @@ __device__ __forceinline__ Sample sample(float sig, float dl) {
 // (1.5 ms forward / 3.3 ms backward at 8,192 x 1,024, latency-bound).
 constexpr int kSeg = 256;  // samples per segment: 4 per lane
 
+// Every staged value is an f16 value (the outputs of h()), so LDS holds them as f16. The
+// serial cumprod / reversed cumsum steps run in native f16 arithmetic: the f32 product of
+// two f16 values is exact, and their f32 sum rounds only where the smaller operand is
+// below a quarter f16 ulp of the larger (both forms then return the larger), so one IEEE
+// f16 multiply / add rounds exactly as h(a * b) / h(a + b) -- one dependent instruction
+// per step of the chain instead of three.
 struct FwdLds {
-  float q2[kSeg], alpha[kSeg], T[kSeg];
-  float t[kMaxC][kSeg];  // f16(f16(color) * w) per band, summed serially
+  _Float16 q2[kSeg], alpha[kSeg], T[kSeg];
+  _Float16 t[kMaxC][kSeg];  // f16(f16(color) * w) per band, summed serially in f32
 };
 
 template <typename T>
@@ -96,36 +102,41 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
   const float* zr = z + b * N;
-  float cp = 1.0f;   // cumprod output, f16 accumulator (cuda scan); lane 0
-  float pr = 1.0f;   // prod over samples, f32 accumulator; lane 0
-  float acc = 0.0f;  // lane c < C: band c's sum over samples, f32 accumulator
+  _Float16 cp = 1.0f;  // cumprod output, f16 accumulator (cuda scan); lane 0
+  float pr = 1.0f;     // prod over samples, f32 accumulator; lane 0
+  float acc = 0.0f;    // lane c < C: band c's sum over samples, f32 accumulator
   for (int s0 = 0; s0 < N; s0 += kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
     for (int li = lane; li < n; li += 64) {
       const Sample sm = sample(h(ld(sigma, b * N + s0 + li)), delta_ref(zr, zs, s0 + li, N));
-      L.q2[li] = sm.q2;
-      L.alpha[li] = sm.alpha;
+      L.q2[li] = static_cast<_Float16>(sm.q2);
+      L.alpha[li] = static_cast<_Float16>(sm.alpha);
     }
     __syncthreads();
     if (lane == 0) {
+#pragma unroll 8
       for (int li = 0; li < n; ++li) {
-        const float q2 = L.q2[li];
+        const _Float16 q2 = L.q2[li];
         L.T[li] = cp;                                   // cumprod(...)[:, :-1]
-        cp = h(cp * q2);
-        pr = pr * q2;                                   // (1 - alpha).prod   (:75)
+        cp = cp * q2;                                   // = h(cp * q2)
+        pr = pr * static_cast<float>(q2);               // (1 - alpha).prod   (:75)
       }
     }
     __syncthreads();
     for (int li = lane; li < n; li += 64) {
       const int64_t i = b * N + s0 + li;
-      const float w = h(L.alpha[li] * L.T[li]);         // alpha * T          (:43-46)
-      for (int c = 0; c < C; ++c) L.t[c][li] = h(h(ld(color, i * C + c)) * w);   // (:48)
+      const float al = static_cast<float>(L.alpha[li]);
+      const float w = h(al * static_cast<float>(L.T[li]));   // alpha * T    (:43-46)
+      for (int c = 0; c < C; ++c)
+        L.t[c][li] = static_cast<_Float16>(h(h(ld(color, i * C + c)) * w));  // (:48)
       if (weights) weights[i] = __float2half_rn(w);
-      if (alpha_out) alpha_out[i] = __float2half_rn(L.alpha[li]);
+      if (alpha_out) alpha_out[i] = __float2half_rn(al);
     }
     __syncthreads();
-    if (lane < C)
-      for (int li = 0; li < n; ++li) acc = acc + L.t[lane][li];
+    if (lane < C) {
+#pragma unroll 8
+      for (int li = 0; li < n; ++li) acc = acc + static_cast<float>(L.t[lane][li]);
+    }
     __syncthreads();
   }
   pr = h(__shfl(pr, 0));
@@ -145,9 +156,9 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
 // phases as fwd_kernel: pass 1 replays the cumprod; pass 2 walks the segments from the
 // last, with the reversed cumsum (rc) as the one serial scan.
 struct BwdLds {
-  float q2[kSeg];
-  float u[kSeg];    // f16(T_k * dL/dT_k): the term sample k adds to rc
-  float rin[kSeg];  // rc before sample k's term: the cumprod backward at k + 1
+  _Float16 q2[kSeg];
+  _Float16 u[kSeg];    // pass 1: T_k; pass 2: f16(T_k * dL/dT_k), the term k adds to rc
+  _Float16 rin[kSeg];  // rc before sample k's term: the cumprod backward at k + 1
 };
 
 template <typename T, typename G>
@@ -170,26 +181,29 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
     csv[c] = (c < C && cs) ? h(ld(cs, b * C + c)) : 0.0f;
   }
   // pass 1: the forward's cumprod outputs (scratch) and the surface product
-  float cp = 1.0f, pr = 1.0f;
+  _Float16 cp = 1.0f;
+  float pr = 1.0f;
   bool zero = false;
   for (int s0 = 0; s0 < N; s0 += kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
     for (int li = lane; li < n; li += 64) {
       const Sample sm = sample(h(ld(sigma, b * N + s0 + li)), delta_ref(zr, zs, s0 + li, N));
-      L.q2[li] = sm.q2;
+      L.q2[li] = static_cast<_Float16>(sm.q2);
       zero = zero || sm.q2 == 0.0f;
     }
     __syncthreads();
     if (lane == 0) {
+#pragma unroll 8
       for (int li = 0; li < n; ++li) {
-        const float q2 = L.q2[li];
+        const _Float16 q2 = L.q2[li];
         L.u[li] = cp;  // T_i, staged for the coalesced scratch store below
-        cp = h(cp * q2);
-        pr = pr * q2;
+        cp = cp * q2;  // = h(cp * q2)
+        pr = pr * static_cast<float>(q2);
       }
     }
     __syncthreads();
-    for (int li = lane; li < n; li += 64) d_sigma[b * N + s0 + li] = static_cast<G>(L.u[li]);
+    for (int li = lane; li < n; li += 64)
+      d_sigma[b * N + s0 + li] = static_cast<G>(static_cast<float>(L.u[li]));
     __syncthreads();
   }
   pr = h(__shfl(pr, 0));
@@ -218,7 +232,7 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
   }
   // pass 2, reverse: reversed cumsum of cp * dL/dcp with an f16 accumulator
   // (cumprod_backward), then each sample's gradients in autograd's order
-  float rc = 0.0f;  // reversed cumsum at j = N: cp_N * 0 (lane 0)
+  _Float16 rc = 0.0f;  // reversed cumsum at j = N: cp_N * 0 (lane 0)
   for (int s0 = ((N - 1) / kSeg) * kSeg; s0 >= 0; s0 -= kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
     float e_[J], dl_[J], q2_[J], gab_[J];
@@ -240,16 +254,17 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
       gw = h(gw);
       gab_[j] = h(gw * Tk);                                       // alpha * T -> alpha
       const float g_T = h(gw * sm.alpha);                         // -> T
-      L.u[li] = h(Tk * g_T);                                      // cp_k * dL/dcp_k
+      L.u[li] = static_cast<_Float16>(h(Tk * g_T));               // cp_k * dL/dcp_k
       e_[j] = sm.e;
       dl_[j] = sm.delta;
       q2_[j] = sm.q2;
     }
     __syncthreads();
     if (lane == 0) {
+#pragma unroll 8
       for (int li = n - 1; li >= 0; --li) {
         L.rin[li] = rc;
-        rc = h(rc + L.u[li]);
+        rc = rc + L.u[li];  // = h(rc + u)
       }
     }
     __syncthreads();
@@ -257,7 +272,7 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
     for (int j = 0; j < J; ++j) {
       const int li = lane + 64 * j;
       if (li >= n) continue;
-      const float g_cpin = h(L.rin[li] / q2_[j]);                // cumprod backward at k+1
+      const float g_cpin = h(static_cast<float>(L.rin[li]) / q2_[j]);  // cumprod bwd at k+1
       const float g_alpha_c = -g_cpin;                            // 1 - alpha + 1e-10
       float g_alpha;
       if (cs) {

@@ -32,6 +32,8 @@ def bwd_chunk(M: int) -> int:
     over = int(os.environ.get("ANR_HASH_KB", "0") or 0)
     if over > 0:
         return over
+    if M >= 512 * 16384:
+        return 512
     return max(1, min(256, M // 4096))
 
 

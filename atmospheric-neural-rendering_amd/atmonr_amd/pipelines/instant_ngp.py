@@ -349,12 +349,24 @@ class _TcnnGradsAtBackwardEnd(torch.autograd.Function):
         def quantize():
             main = torch.cuda.current_stream(dev)
             main.wait_stream(_lib.side_stream(dev))
+            grads = []
             for m in pipe.modules():
                 p = m.params
                 if p.numel() and p.grad is not None:
                     if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
                         raise _lib.ANRError("reference numerics: f32 contiguous grads only")
-                    _lib.call("anr_grad_quantize_f16", _lib.ptr(p.grad), p.grad.numel(),
-                              float(pipe.loss_scale), _lib.stream(dev), tag="grad_quantize")
+                    grads.append(p.grad)
+            # gradients that tile one contiguous range (a FlatGradBucket's views) are
+            # quantised in one launch (elementwise: the same values)
+            grads.sort(key=lambda g: g.data_ptr())
+            spans = []
+            for g in grads:
+                if spans and spans[-1][0] + 4 * spans[-1][1] == g.data_ptr():
+                    spans[-1][1] += g.numel()
+                else:
+                    spans.append([g.data_ptr(), g.numel()])
+            for base, n in spans:
+                _lib.call("anr_grad_quantize_f16", base, n, float(pipe.loss_scale),
+                          _lib.stream(dev), tag="grad_quantize")
         torch.autograd.Variable._execution_engine.queue_callback(quantize)
         return g, None

@@ -204,7 +204,6 @@ _SIGNATURES = {
     "anr_ingp_field_supported": (c_int32, [POINTER(MlpDesc), POINTER(MlpDesc)]),
     "anr_ingp_field_packed_size": (c_int64, [POINTER(MlpDesc), POINTER(MlpDesc)]),
     "anr_ingp_field_set_grad_scale": (c_int32, [c_int32]),
-    "anr_ingp_field_force_bwd": (c_int32, [c_int32]),
     "anr_ingp_field_force_fwd": (c_int32, [c_int32]),
     "anr_ingp_field_bwd_workspace_bytes": (
         c_int64, [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, c_int64]),

@@ -796,351 +796,11 @@ __device__ __forceinline__ void raw_to_rows(const RawRows& r, int g, Rows& in) {
   in.dc = g == 0 ? r.dc : z4;
 }
 
-template <int W, int NHD, bool FAST, bool ROWS, bool BF>
-__global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t tpw,
-                                                  const float* wmax) {
-  using N = Net<W, NHD>;
-  constexpr int NT = N::NT, KB = N::KB, LX = N::LX, LH = N::LH;
-  // Three separate LDS objects, so alias analysis can tell weight-fragment reads, layer-
-  // input tiles and gradient tiles apart and keep reads in flight across the others' stores.
-  __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
-  __shared__ __attribute__((aligned(16))) _Float16 xsm[4][N::wave_x];
-  __shared__ __attribute__((aligned(16))) _Float16 gsm[4][N::wave_g];
-  _Float16* wb = wsm;
-  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
-  const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
-  for (int e = threadIdx.x * 8; e < N::n_packed; e += blockDim.x * 8)
-    *reinterpret_cast<h8*>(wb + e) = *reinterpret_cast<const h8*>(a.packed + e);
-  _Float16* Xpe = xsm[wave] + N::oXpe;
-  _Float16* Xph = xsm[wave] + N::oXph;
-  _Float16* Xde = xsm[wave] + N::oXde;
-  _Float16* Xd0 = xsm[wave] + N::oXd0;
-  _Float16* Xd1 = xsm[wave] + N::oXd1;
-  _Float16* Ga = gsm[wave] + N::oGa;
-  _Float16* Gb = gsm[wave] + N::oGb;
-  _Float16* Xlast = NHD == 2 ? Xd1 : Xd0;
-  __syncthreads();
-  // wbt: per-tile opaque copy of the fragment base, so the compiler re-reads the weight
-  // fragments from LDS each tile instead of hoisting them into registers
-  const _Float16* wbt = wb;
-  auto bfrag32 = [&](int off) { return *reinterpret_cast<const h8*>(wbt + off + lane * 8); };
-  auto bfrag16 = [&](int off) { return *reinterpret_cast<const h4*>(wbt + off + lane * 4); };
-
-  const int64_t n_tiles = (a.M + 31) / 32;
-  const int64_t w_id = static_cast<int64_t>(blockIdx.x) * waves + wave;
-  const int64_t t_begin = w_id * tpw;
-  const int64_t t_end = t_begin + tpw < n_tiles ? t_begin + tpw : n_tiles;
-  const int64_t n_full = a.M / 32;  // tiles with all 32 rows in range
-
-  f4 dD2[NT], dD1[NHD == 2 ? NT * NT : 1], dD0[NT * 2], dP1[NT], dP0[NT * 2];
-  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int i = 0; i < NT; ++i) dD2[i] = dP1[i] = z4;
-#pragma unroll
-  for (int i = 0; i < NT * 2; ++i) dD0[i] = dP0[i] = z4;
-  if constexpr (NHD == 2) {
-#pragma unroll
-    for (int i = 0; i < NT * NT; ++i) dD1[i] = z4;
-  }
-  // f16 gradient scale 2^e of this wavefront (max over its rows -> target); the dW
-  // accumulators are never touched by VALU inside the tile loop (they stay in AGPRs)
-  float s = 1.0f, inv_s = 1.0f;
-  if constexpr (!BF) {  // bf16 has f32's exponent range: no scaling
-    const float gm = wave_grad_max(a, wmax, w_id, t_begin, t_end);
-    if (gm > 0.0f) {
-      int e = static_cast<int>(floorf(log2f(target / gm)));
-      e = e < -60 ? -60 : (e > 100 ? 100 : e);
-      s = ldexpf(1.0f, e);
-      inv_s = ldexpf(1.0f, -e);
-    }
-  }
-
-  Rows cur[2];
-  RawRows nraw[2];
-  const int64_t t_full_end = t_end < n_full ? t_end : n_full;
-  if constexpr (FAST) {
-    if (t_begin < t_full_end) {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, t_begin * 32 + mt * 16 + li, g, nraw[mt]);
-    }
-  }
-#ifdef FIELD_STAMP
-  const bool stamp_on = w_id == 0;
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
-  {
-    unsigned long long t_;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));
-    st_last = t_;
-  }
-#endif
-  // one tile; FULL: all 32 rows in range (no bounds checks, one basic block)
-  auto process = [&](auto full_c, int64_t tile) {
-    constexpr bool FULL = decltype(full_c)::value;
-    {
-      int zoff = 0;
-      asm volatile("" : "+v"(zoff));
-      wbt = wb + zoff;
-    }
-    if constexpr (FAST && FULL) {
-      // this tile's inputs arrived during the previous tile; issue the next tile's now
-      // (clamped to the last full tile: always a valid address, no branch)
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) raw_to_rows(nraw[mt], g, cur[mt]);
-      const int64_t tn = tile + 1 < t_full_end ? tile + 1 : tile;
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_raw<ROWS>(a, tn * 32 + mt * 16 + li, g, nraw[mt]);
-    } else {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) load_rows<ROWS>(a, tile * 32 + mt * 16 + li, g, true, cur[mt]);
-    }
-    const bool full = FULL;
-    STAMP(0);
-    h4 gc[2];
-    bool dens[2];
-    // ---- recompute the forward for both 16-sample halves; every layer input goes to LDS
-    // as soon as it is computed (the backward's ReLU masks are read back from there)
-    {
-      Tile<W, NHD> t[2];
-      bool valid[2];
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) valid[mt] = full || tile * 32 + mt * 16 + li < a.M;
-      struct Sink {
-        _Float16 *Xpe, *Xde, *Xph, *Xd0, *Xd1;
-        int li, g;
-        __device__ void xe(int mt, h8 v) const { if constexpr ((FIELD_EXP & 2) == 0) *reinterpret_cast<h8*>(Xpe + (mt * 16 + li) * LX + 8 * g) = v; }
-        __device__ void xd(int mt, h8 v) const { if constexpr ((FIELD_EXP & 2) == 0) *reinterpret_cast<h8*>(Xde + (mt * 16 + li) * LX + 8 * g) = v; }
-        __device__ void hp(int mt, int nt, h4 v) const { if constexpr ((FIELD_EXP & 2) == 0) st4(Xph, LH, mt * 16 + li, 16 * nt + 4 * g, v); }
-        __device__ void hd0(int mt, int nt, h4 v) const { if constexpr ((FIELD_EXP & 2) == 0) st4(Xd0, LH, mt * 16 + li, 16 * nt + 4 * g, v); }
-        __device__ void hd1(int mt, int nt, h4 v) const { if constexpr ((FIELD_EXP & 2) == 0) st4(Xd1, LH, mt * 16 + li, 16 * nt + 4 * g, v); }
-      };
-      // all forward fragments in flight at once, then the five layers
-      FwdWeights<W, NHD> fwl;
-      fwl.load(wbt, lane);
-      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
-      tile_forward<W, NHD, 2, BF>(fwl, cur, valid, g, t, Sink{Xpe, Xde, Xph, Xd0, Xd1, li, g});
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        dens[mt] = t[mt].po[0] > 0.0f;
-        f4 gv;  // dL/d(color pre-activation), scaled (cur.dc is zero outside g == 0)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) gv[i] = t[mt].col[i] > 0.0f ? cur[mt].dc[i] * s : 0.0f;
-        gc[mt] = to_h4<BF>(gv);
-        st4g(Ga, LH, mt * 16 + li, 4 * g, gc[mt]);
-      }
-    }
-    STAMP(1);
-    // Each stage below first issues every LDS read it needs (weight fragments, ReLU masks,
-    // transposed tiles), then a scheduling barrier, then its MFMAs: one LDS round trip
-    // per stage instead of one per MFMA group.
-    // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
-    h4 dl[2][NT];
-    {
-      const h8 ga = tr_read(Ga, LH, 0, lane);
-      h8 xl[NT];
-      h4 wf[NT], mk[2][NT];
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-        xl[kt] = tr_read(Xlast, LH, 16 * kt, lane);
-        wf[kt] = bfrag16(N::oBD2 + kt * N::F16);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xlast, LH, mt * 16 + li, 16 * kt + 4 * g);
-      }
-      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) mma32_acc<BF>(dD2[kt], ga, xl[kt]);
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          dl[mt][kt] = mask_h4<BF>(mma16<BF>(wf[kt], gc[mt], z4), mk[mt][kt]);
-          st4g(Gb, LH, mt * 16 + li, 16 * kt + 4 * g, dl[mt][kt]);
-        }
-      }
-    }
-    STAMP(2);
-    // ---- dir hidden layer 1 (NHD == 2): dW_D1 (W x W) += dl^T · X_d0 ; dh0 = D1^T dl
-    h4 dh0[2][NT];
-    _Float16* Gdh0 = Gb;
-    if constexpr (NHD == 2) {
-      h8 xb[NT], gb[NT], wf[NT * KB];
-      h4 mk[2][NT];
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-        xb[kt] = tr_read(Xd0, LH, 16 * kt, lane);
-        gb[kt] = tr_read(Gb, LH, 16 * kt, lane);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) wf[kt * KB + kb] = bfrag32(N::oBD1 + (kt * KB + kb) * N::F32);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xd0, LH, mt * 16 + li, 16 * kt + 4 * g);
-      }
-      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int kt = 0; kt < NT; ++kt) mma32_acc<BF>(dD1[nt * NT + kt], gb[nt], xb[kt]);
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-        f4 acc[2] = {z4, z4};
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf[kt * KB + kb], cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          dh0[mt][kt] = mask_h4<BF>(acc[mt], mk[mt][kt]);
-          st4g(Ga, LH, mt * 16 + li, 16 * kt + 4 * g, dh0[mt][kt]);
-        }
-      }
-      Gdh0 = Ga;
-    } else {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int kt = 0; kt < NT; ++kt) dh0[mt][kt] = dl[mt][kt];
-    }
-    _Float16* Gfree = NHD == 2 ? Gb : Ga;
-    STAMP(3);
-    // ---- dir input layer: dW_D0 (W x 32, k' order) += dh0^T · X_de ; dpos = D0^T dh0
-    h4 dpo[2];
-    {
-      const h8 x0 = tr_read(Xde, LX, 0, lane), x1 = tr_read(Xde, LX, 16, lane);
-      h8 gd[NT], wf[KB];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) gd[nt] = tr_read(Gdh0, LH, 16 * nt, lane);
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) wf[kb] = bfrag32(N::oBD0 + kb * N::F32);
-      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        mma32_acc<BF>(dD0[nt * 2], gd[nt], x0);
-        mma32_acc<BF>(dD0[nt * 2 + 1], gd[nt], x1);
-      }
-      f4 acc[2] = {z4, z4};
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf[kb], cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        // pos_out[:, 0] is the density: its gradient is dL/dsigma through the ReLU
-        const float dsv = dens[mt] ? cur[mt].ds * s : 0.0f;
-        acc[mt][0] = g == 0 ? dsv : acc[mt][0];
-        dpo[mt] = to_h4<BF>(acc[mt]);
-        st4g(Gfree, LH, mt * 16 + li, 4 * g, dpo[mt]);
-      }
-    }
-    STAMP(4);
-    // ---- pos output layer: dW_P1 (16 x W) += dpo^T · X_ph ; dhp = P1^T dpo
-    h4 dhp[2][NT];
-    {
-      const h8 ga = tr_read(Gfree, LH, 0, lane);
-      h8 xp[NT];
-      h4 wf[NT], mk[2][NT];
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-        xp[kt] = tr_read(Xph, LH, 16 * kt, lane);
-        wf[kt] = bfrag16(N::oBP1 + kt * N::F16);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) mk[mt][kt] = ld4(Xph, LH, mt * 16 + li, 16 * kt + 4 * g);
-      }
-      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) mma32_acc<BF>(dP1[kt], ga, xp[kt]);
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          dhp[mt][kt] = mask_h4<BF>(mma16<BF>(wf[kt], dpo[mt], z4), mk[mt][kt]);
-          st4g(Gdh0, LH, mt * 16 + li, 16 * kt + 4 * g, dhp[mt][kt]);
-        }
-      }
-    }
-    STAMP(5);
-    // ---- pos input layer: dW_P0 (W x 32) += dhp^T · X_pe ; d_enc = P0^T dhp
-    {
-      const h8 x0 = tr_read(Xpe, LX, 0, lane), x1 = tr_read(Xpe, LX, 16, lane);
-      h8 gp[NT], wf[2 * KB];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) gp[nt] = tr_read(Gdh0, LH, 16 * nt, lane);
-#pragma unroll
-      for (int i = 0; i < 2 * KB; ++i) wf[i] = bfrag32(N::oBP0 + i * N::F32);
-      __builtin_amdgcn_sched_barrier(FIELD_STAGE_MASK);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        mma32_acc<BF>(dP0[nt * 2], gp[nt], x0);
-        mma32_acc<BF>(dP0[nt * 2 + 1], gp[nt], x1);
-      }
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        f4 acc[2] = {z4, z4};
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) acc[mt] = mma32<BF>(wf[kt * KB + kb], cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int64_t row = tile * 32 + mt * 16 + li;
-          if (full || row < a.M) {
-            const f4 v = acc[mt] * inv_s;
-            *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
-          }
-        }
-      }
-    }
-    STAMP(6);
-    // see mma32_acc_v: no loop-exit copy of an accumulator while an MFMA still writes it
-    agpr_fence();
-    agpr_pin(dD2);
-    agpr_pin(dD1);
-    agpr_pin(dD0);
-    agpr_pin(dP1);
-    agpr_pin(dP0);
-  };
-  for (int64_t tile = t_begin; tile < t_full_end; ++tile) process(std::integral_constant<bool, true>{}, tile);
-  for (int64_t tile = t_full_end > t_begin ? t_full_end : t_begin; tile < t_end; ++tile)
-    process(std::integral_constant<bool, false>{}, tile);
-
-#ifdef FIELD_STAMP
-  if (stamp_on && lane == 0) {
-    for (int k = 0; k < 8; ++k) g_stamp[k] = st_acc[k];
-    g_stamp[8] = static_cast<unsigned long long>(t_end - t_begin);
-  }
-#endif
-  agpr_fence();
-  agpr_pin(dD2);
-  agpr_pin(dD1);
-  agpr_pin(dD0);
-  agpr_pin(dP1);
-  agpr_pin(dP0);
-  // ---- flush: lane holds dW[n = 16·ntile + 4g + i][k = 16·ktile + li]
-  auto flush = [&](float* dst, int ld, const f4& d, int n0, int k) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (d[i] != 0.0f) atomicAdd(dst + (n0 + 4 * g + i) * ld + k, d[i] * inv_s);
-  };
-#pragma unroll
-  for (int kt = 0; kt < NT; ++kt) {
-    flush(a.g_dir + N::D2, W, dD2[kt], 0, 16 * kt + li);
-    flush(a.g_pos + N::P1, W, dP1[kt], 0, 16 * kt + li);
-  }
-  if constexpr (NHD == 2) {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) flush(a.g_dir + N::D1, W, dD1[nt * NT + kt], 16 * nt, 16 * kt + li);
-  }
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      flush(a.g_dir + N::D0, 32, dD0[nt * 2 + kt], 16 * nt, dir_col(16 * kt + li));
-      flush(a.g_pos + N::P0, 32, dP0[nt * 2 + kt], 16 * nt, 16 * kt + li);
-    }
-}
-
 // ---------------------------------------------------------------------------------
-// Backward v2, register-transposed: the same math and flush as bwd_kernel, but no layer
-// input or gradient tile goes through LDS (LDS holds only the packed weights).
+// Backward, register-transposed: no layer input or gradient tile goes through LDS (LDS
+// holds the packed weights and the block's dW sums). (The r01 generation that staged
+// every tile in LDS and read it back with ds_read_b64_tr_b16, and r03's variant with only
+// the dW operand transposes through LDS, were A/B generations; removed in r04.)
 //
 // dW += G^T · X contracts over the samples, so both operands need the samples along K
 // (lane = unit, samples in the lane's registers) while the chain holds every tile with
@@ -1152,7 +812,7 @@ __global__ void __launch_bounds__(256) bwd_kernel(Args a, float target, int64_t 
 // input) go through a 16x16x32 MFMA against [I|0] or [0|I]. The dW A operand of a
 // 32-sample tile is then cat(transpose(half 0), transpose(half 1)), i.e. samples in the
 // order (4g..4g+3, 16+4g..16+4g+3) along K, and the B operand the same: the contraction
-// is order-blind, and the accumulator layout (and with it the flush) is bwd_kernel's.
+// is order-blind.
 // ReLU masks are the forward's activations, kept in registers.
 // ---------------------------------------------------------------------------------
 template <bool BF>
@@ -1181,32 +841,6 @@ __device__ __forceinline__ h4 tr_b(h8 x, h8 sel) {
   return to_h4<BF>(mma32<BF>(x, sel, f4{0.0f, 0.0f, 0.0f, 0.0f}));
 }
 
-// The same transposes through a wave-private LDS image (LT): each lane stores its 4 (C
-// tile) or 8 (B-operand tile) 16-bit values as one row piece, and ds_read_b64_tr_b16 hands
-// lane (g, c) column c of rows 4g..4g+3 — the layout tr_c / tr_b produce, bit for bit,
-// without the MFMA, its two f32 -> 16-bit conversions and their result wait states.
-// C tile: 16 rows (samples) x 16 units, 32-B rows, 8-B piece c of row r at c ^ (r >> 2):
-// the b64 writes (32 banks) and the transposed reads (64 banks, 32-lane halves) are both
-// conflict-free. B tile: 16 rows x 32 slots, 64-B rows, 16-B piece c of row r at
-// c ^ (2 * ((r >> 2) & 1)), so a 32-lane half's transposed read covers 64 distinct banks.
-__device__ __forceinline__ void lt_put_c(_Float16* img, int g, int li, h4 v) {
-  *reinterpret_cast<h4*>(img + li * 16 + 4 * (g ^ (li >> 2))) = v;
-}
-__device__ __forceinline__ h4 lt_get_c(const _Float16* img, int g, int li) {
-  const _Float16* p = img + (4 * g + (li >> 2)) * 16 + 4 * ((li & 3) ^ g);
-  return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p)));
-}
-__device__ __forceinline__ void lt_put_b(_Float16* img, int g, int li, h8 v) {
-  *reinterpret_cast<h8*>(img + li * 32 + 8 * (g ^ ((li >> 1) & 2))) = v;
-}
-// slots 16kb .. 16kb+15 of the B tile, transposed (= tr_b(x, sel[kb]))
-__device__ __forceinline__ h4 lt_get_b(const _Float16* img, int kb, int g, int li) {
-  const int r = 4 * g + (li >> 2), p = li & 3;
-  const _Float16* q = img + r * 32 + 8 * ((2 * kb + (p >> 1)) ^ ((r >> 1) & 2)) + 4 * (p & 1);
-  return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(q)));
-}
-constexpr int kLtSlot = 256;     // f16 elements of one C-tile image (a B tile takes two)
-constexpr int kLtRegion = 16;    // slots of one layer's transposes (32-sample tiles)
 
 // REF (reference numerics, f16 only): the gradient scale is tcnn's fixed loss scale
 // (a.loss_scale = 128) instead of the per-wavefront power of two, the ReLU masks test the
@@ -1215,8 +849,7 @@ constexpr int kLtRegion = 16;    // slots of one layer's transposes (32-sample t
 // dir_encoder as f16(f16(g_scaled) / 128) (a subnormal-flushing f16 division) and is
 // rescaled for pos_mlp, and dL/denc is written as f16(f16(g_scaled) / 128)
 // (tinycudann/modules.py: input_grad / loss_scale, cast to the f16 input's dtype).
-// LT: the dW operand transposes through LDS (lt_put_* / lt_get_*) instead of MFMAs.
-template <int W, int NHD, bool FAST, bool ROWS, bool BF, bool REF = false, bool LT = false>
+template <int W, int NHD, bool FAST, bool ROWS, bool BF, bool REF = false>
 __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64_t tpw,
                                                      const float* wmax) {
   static_assert(!(REF && BF), "reference numerics are f16");
@@ -1226,8 +859,6 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   using N = Net<W, NHD>;
   constexpr int NT = N::NT, KB = N::KB;
   __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
-  // 4 wavefronts x two alternating regions (consecutive layers' transposes may overlap)
-  __shared__ __attribute__((aligned(16))) _Float16 trs[LT ? 4 * 2 * kLtRegion * kLtSlot : 8];
   // the block's dW partials (pos parameters, then dir), summed here before the one global
   // flush per block
   __shared__ float red[N::NPOS + N::NDIR];
@@ -1244,29 +875,14 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   auto bfrag16 = [&](int off) { return *reinterpret_cast<const h4*>(wbt + off + lane * 4); };
   TrConst<BF> tc;
   tc.init(lane);
-  _Float16* const trw = trs + (LT ? wave * 2 * kLtRegion * kLtSlot : 0);
-  // dW operand transposes; `slot` (region * kLtRegion + index) names the LDS image (LT)
-  auto trc = [&](int slot, h4 x) -> h4 {
-    if constexpr (LT) {
-      _Float16* img = trw + slot * kLtSlot;
-      lt_put_c(img, g, li, x);
-      return lt_get_c(img, g, li);
-    } else {
-      return tr_c<BF>(x, tc.id);
-    }
+  // dW operand transposes (MFMA against the constant 0/1 operands); the slot argument
+  // names the r03 LDS image of the removed LT generation and is unused
+  auto trc = [&](int, h4 x) -> h4 { return tr_c<BF>(x, tc.id); };
+  auto trb = [&](int, h8 x, h4& o0, h4& o1) {
+    o0 = tr_b<BF>(x, tc.sel[0]);
+    o1 = tr_b<BF>(x, tc.sel[1]);
   };
-  auto trb = [&](int slot, h8 x, h4& o0, h4& o1) {
-    if constexpr (LT) {
-      _Float16* img = trw + slot * kLtSlot;
-      lt_put_b(img, g, li, x);
-      o0 = lt_get_b(img, 0, g, li);
-      o1 = lt_get_b(img, 1, g, li);
-    } else {
-      o0 = tr_b<BF>(x, tc.sel[0]);
-      o1 = tr_b<BF>(x, tc.sel[1]);
-    }
-  };
-  constexpr int R0 = 0, R1 = kLtRegion;
+  constexpr int R0 = 0, R1 = 16;
 
   const int64_t n_tiles = (a.M + TR - 1) / TR;
   const int64_t w_id = static_cast<int64_t>(blockIdx.x) * waves + wave;
@@ -1614,10 +1230,6 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
 // host side
 // ---------------------------------------------------------------------------------
 static int g_target_log2 = 6;  // f16 gradient scale: max |dL/dout| of a wavefront -> 2^6
-// backward kernel generation: 0 = LDS tiles (bwd_kernel), 1 = register-transposed
-// (bwd_rt_kernel, MFMA transposes), 2 = the same with the transposes through LDS (LT);
-// test / A-B hook anr_ingp_field_force_bwd
-static int g_bwd_mode = 1;
 // forward form: 1 = the uniform-tile kernel where the shapes allow (default), 0 = always
 // the general kernel; test / A-B hook anr_ingp_field_force_fwd
 static int g_fwd_ut = 1;
@@ -1629,24 +1241,18 @@ struct BwdGeom {
   int64_t blocks, nw, tpw;
 };
 template <int W, int NHD, bool BF>
-static const void* bwd_fn(bool fast, int mode) {
-  if (mode == 1)
-    return fast ? reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, true, false, BF>)
-                : reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, false, false, BF>);
-  if (mode == 2)
-    return fast ? reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, true, false, BF, false, true>)
-                : reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, false, false, BF, false, true>);
-  return fast ? reinterpret_cast<const void*>(&bwd_kernel<W, NHD, true, false, BF>)
-              : reinterpret_cast<const void*>(&bwd_kernel<W, NHD, false, false, BF>);
+static const void* bwd_fn(bool fast) {
+  return fast ? reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, true, false, BF>)
+              : reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, false, false, BF>);
 }
 template <int W, int NHD, bool BF>
-static BwdGeom bwd_geom(int64_t M, bool fast, int mode) {
+static BwdGeom bwd_geom(int64_t M, bool fast) {
   const int waves = 4;
-  static int pc[3][2] = {{0, 0}, {0, 0}, {0, 0}};
-  int& p = pc[mode][fast ? 1 : 0];
+  static int pc[2] = {0, 0};
+  int& p = pc[fast ? 1 : 0];
   if (p == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, bwd_fn<W, NHD, BF>(fast, mode), 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, bwd_fn<W, NHD, BF>(fast), 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
     p = nb;
   }
   const int64_t tiles = (M + 31) / 32;
@@ -1660,14 +1266,13 @@ static BwdGeom bwd_geom(int64_t M, bool fast, int mode) {
 template <int W, int NHD, bool BF>
 static int64_t bwd_workspace(int64_t M) {
   if (BF || M <= 0) return 0;
-  // the largest wave count of the backward kernels (both generations, fast and general
-  // d_color layouts), so a workspace sized once serves whichever runs
+  // the larger wave count of the fast and general d_color layouts, so a workspace sized
+  // once serves whichever runs
   int64_t n = 0;
-  for (int mode = 0; mode < 3; ++mode)
-    for (int f = 0; f < 2; ++f) {
-      const int64_t w = bwd_geom<W, NHD, BF>(M, f == 1, mode).nw;
-      n = w > n ? w : n;
-    }
+  for (int f = 0; f < 2; ++f) {
+    const int64_t w = bwd_geom<W, NHD, BF>(M, f == 1).nw;
+    n = w > n ? w : n;
+  }
   return static_cast<int64_t>(sizeof(float)) * n;
 }
 
@@ -1708,7 +1313,7 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
       return 1;
     } else {
       if (a.rows) return 1;
-      const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast, 1);
+      const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast);
       const dim3 grid(static_cast<unsigned>(gm.blocks)), block(64 * waves);
       if (fast)
         hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, true, false, false, true>), grid, block, 0, st, a,
@@ -1719,12 +1324,9 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
       return 0;
     }
   }
-  const int mode = g_bwd_mode;
-  const size_t lds = (static_cast<size_t>(N::n_packed) + (mode == 0 ? waves * N::wave_lds : 0) +
-                      (mode == 2 ? 4 * 2 * kLtRegion * kLtSlot : 0)) * 2 +
-                     (mode != 0 ? sizeof(float) * (N::NPOS + N::NDIR) : 0);
+  const size_t lds = static_cast<size_t>(N::n_packed) * 2 + sizeof(float) * (N::NPOS + N::NDIR);
   if (lds > 160 * 1024) return 1;
-  const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast, mode);
+  const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast);
   if (!BF && (ws == nullptr || ws_bytes < static_cast<int64_t>(sizeof(float)) * gm.nw))
     return 2;
   const float target = ldexpf(1.0f, g_target_log2);
@@ -1735,32 +1337,15 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
     else
       hipLaunchKernelGGL(absmax_kernel<false>, dim3(gm.nw), dim3(1024), 0, st, a, gm.tpw * 32, ws);
   }
-#define ANR_BWD_LAUNCH(K, FASTV, ROWSV) \
-  hipLaunchKernelGGL((K<W, NHD, FASTV, ROWSV, BF>), grid, block, 0, st, a, target, gm.tpw, ws)
-#define ANR_BWD_LAUNCH_LT(FASTV, ROWSV)                                                        \
-  hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, FASTV, ROWSV, BF, false, true>), grid, block, 0, st, \
-                     a, target, gm.tpw, ws)
-  if (mode == 2) {
-    if (a.rows) {
-      if (fast) ANR_BWD_LAUNCH_LT(true, true); else ANR_BWD_LAUNCH_LT(false, true);
-    } else {
-      if (fast) ANR_BWD_LAUNCH_LT(true, false); else ANR_BWD_LAUNCH_LT(false, false);
-    }
-  } else if (mode == 1) {
-    if (a.rows) {
-      if (fast) ANR_BWD_LAUNCH(bwd_rt_kernel, true, true); else ANR_BWD_LAUNCH(bwd_rt_kernel, false, true);
-    } else {
-      if (fast) ANR_BWD_LAUNCH(bwd_rt_kernel, true, false); else ANR_BWD_LAUNCH(bwd_rt_kernel, false, false);
-    }
+#define ANR_BWD_LAUNCH(FASTV, ROWSV) \
+  hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, FASTV, ROWSV, BF>), grid, block, 0, st, a, target, \
+                     gm.tpw, ws)
+  if (a.rows) {
+    if (fast) ANR_BWD_LAUNCH(true, true); else ANR_BWD_LAUNCH(false, true);
   } else {
-    if (a.rows) {
-      if (fast) ANR_BWD_LAUNCH(bwd_kernel, true, true); else ANR_BWD_LAUNCH(bwd_kernel, false, true);
-    } else {
-      if (fast) ANR_BWD_LAUNCH(bwd_kernel, true, false); else ANR_BWD_LAUNCH(bwd_kernel, false, false);
-    }
+    if (fast) ANR_BWD_LAUNCH(true, false); else ANR_BWD_LAUNCH(false, false);
   }
 #undef ANR_BWD_LAUNCH
-#undef ANR_BWD_LAUNCH_LT
   return 0;
 }
 
@@ -1835,12 +1420,6 @@ extern "C" int64_t anr_ingp_field_bwd_workspace_bytes(const anr_mlp_desc* pos,
     case 642: return bwd_workspace<64, 2, false>(M);
   }
   return 0;
-}
-
-extern "C" int anr_ingp_field_force_bwd(int32_t mode) {
-  const int prev = g_bwd_mode;
-  if (mode >= 0 && mode <= 2) g_bwd_mode = mode;
-  return prev;
 }
 
 extern "C" int anr_ingp_field_force_fwd(int32_t mode) {

@@ -625,10 +625,6 @@ def main():
                          "deviation that trains differently, DESIGN.md §3.1); the other one "
                          "is timed after it unless --no-alt-numerics")
     ap.add_argument("--no-alt-numerics", action="store_true")
-    ap.add_argument("--field-bwd", choices=["rt", "rt_lt", "lds"], default="rt",
-                    help="fused field backward generation (anr_ingp_field_force_bwd): "
-                         "register-transposed (default), the same with the dW operand "
-                         "transposes through LDS, or LDS-staged tiles")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every kernel timed (per-kernel breakdown)")
     args = ap.parse_args()
@@ -662,7 +658,6 @@ def main():
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
     from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
 
-    _lib.load().anr_ingp_field_force_bwd({"lds": 0, "rt": 1, "rt_lt": 2}[args.field_bwd])
     t0 = time.time()
     ds = SyntheticHARP2Dataset(n_views=args.views, img_size=args.img_size, device=dev, seed=0)
     torch.cuda.synchronize()

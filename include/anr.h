@@ -267,12 +267,6 @@ int64_t anr_ingp_field_packed_size(const anr_mlp_desc* pos, const anr_mlp_desc* 
 /* f16 gradient scale target of the backward (max |dL/dout| per wavefront -> 2^v);
  * returns the previous value. Test hook; process-wide. */
 int anr_ingp_field_set_grad_scale(int32_t log2_target);
-/* Backward kernel generation: 0 = layer inputs and gradient tiles staged in LDS, 1 =
- * register-transposed (default; transposes by MFMA against a 0/1 matrix, LDS holds only
- * the weights), 2 = register-transposed with the dW operand transposes through LDS
- * (ds_read_b64_tr_b16). Same math; bit-identical dL/denc. Test / A-B hook; process-wide;
- * other values keep the current mode. Returns the previous mode. */
-int anr_ingp_field_force_bwd(int32_t mode);
 /* Forward kernel form: 1 = the uniform-tile form wherever the shapes allow it (default:
  * dense rows, samples_per_ray a multiple of 16, 4 colour outputs, 16-byte aligned colour
  * rows; one scalar direction load per 16-row tile, branch-free output stores), 0 = always

@@ -693,26 +693,11 @@ def _field_preacts(enc, dirs, n_per_ray, pp, pd, width, nhd, half=True):
     return torch.stack(mins, 1).min(1).values
 
 
-# field backward generations (anr_ingp_field_force_bwd): "rt" = register-transposed
-# (default), "rt_lt" = the same with the dW operand transposes through LDS, "lds" =
-# layer inputs / gradient tiles staged in LDS
-_BWD_MODES = {"lds": 0, "rt": 1, "rt_lt": 2}
-
-
-@pytest.fixture(params=["rt", "rt_lt", "lds"])
-def field_bwd_mode(request):
-    from atmonr_amd import _lib
-
-    prev = _lib.load().anr_ingp_field_force_bwd(_BWD_MODES[request.param])
-    yield request.param
-    _lib.load().anr_ingp_field_force_bwd(prev)
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("mma", ["f16", "bf16"])
 @pytest.mark.parametrize("width,nhd,R", [(64, 2, 29), (64, 2, 300), (32, 2, 29), (64, 1, 29),
                                          (32, 1, 31)])
-def test_ingp_field_matches_oracle(dev, field_bwd_mode, width, nhd, R, mma):
+def test_ingp_field_matches_oracle(dev, width, nhd, R, mma):
     """anr_ingp_field_{pack,fwd,bwd} == pos MLP -> SH2|pos_out[:,1:] -> dir MLP (oracle),
     with the oracle rounding operands where the kernel does: f16 (the reference's tcnn
     precision) or bf16 (BASELINE configs[4]). Tolerances (relative to the largest value):
@@ -811,73 +796,16 @@ def test_ingp_field_unsupported_and_empty(dev):
 
 
 @pytest.mark.parametrize("mma", ["f16", "bf16"])
-@pytest.mark.parametrize("width,nhd", [(64, 2), (32, 1)])
-def test_ingp_field_bwd_generations_agree(dev, width, nhd, mma):
-    """The register-transposed backward (mode 1), the same with LDS transposes (mode 2) and
-    the LDS-tile backward (mode 0) on the same inputs (256 rays x 1024 samples plus a
-    ragged 77-row tail). bf16 (unscaled): d_enc bit-identical (the dX chain is the same
-    MFMA sequence on the same operands; the transposes are exact), parameter gradients
-    within 1e-5 relative L2 (mode 0's dW contraction visits the 32 samples of a tile in a
-    different K order, and the flush is atomic). f16: each wavefront scales its gradients
-    by a power of two set from its own rows, and the row-to-wavefront partition follows
-    each kernel's occupancy, so where two generations differ in occupancy the scales, and
-    with them which tiny gradients flush to f16 zero, differ: within 1e-4 relative L2."""
-    from atmonr_amd import _lib
-
-    nb, R, n_per_ray = 4, 256, 1024
-    M = R * n_per_ray + 77
-    code = _lib.BF16 if mma == "bf16" else _lib.F16
-    g = torch.Generator(device=dev).manual_seed(21)
-    lib = _lib.load()
-    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
-    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
-    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
-    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
-    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
-    dirs = torch.rand(R + 1, 3, device=dev, generator=g)
-    s = _lib.stream(dev)
-    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
-    _lib.call("anr_ingp_field_pack", pb, db, code, pp.data_ptr(), pd.data_ptr(),
-              packed.data_ptr(), s)
-    dcol = torch.randn(M, nb, device=dev, generator=g) * 1e-3
-    dsig = torch.randn(M, device=dev, generator=g) * 1e-3
-    ws_bytes = lib.anr_ingp_field_bwd_workspace_bytes(pb, db, code, M)
-    ws = torch.empty(max(1, ws_bytes // 4), device=dev)
-    out = {}
-    for mode in (0, 1, 2):
-        prev = lib.anr_ingp_field_force_bwd(mode)
-        try:
-            d_enc = torch.full((M, 32), float("nan"), device=dev)
-            g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
-            _lib.call("anr_ingp_field_bwd", pb, db, code, packed.data_ptr(), enc.data_ptr(), 32,
-                      dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
-                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(),
-                      ws.data_ptr() if ws_bytes else None, ws_bytes, s)
-            torch.cuda.synchronize(dev)
-        finally:
-            lib.anr_ingp_field_force_bwd(prev)
-        out[mode] = (d_enc, g_pos, g_dir)
-    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
-    for m in (0, 2):
-        if mma == "bf16":
-            assert torch.equal(out[m][0], out[1][0]), m
-        else:
-            assert rel(out[m][0], out[1][0]) <= 1e-4, m
-        for i in (1, 2):
-            assert rel(out[m][i], out[1][i]) <= (1e-5 if mma == "bf16" else 1e-4), (m, i)
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("mma", ["f16", "bf16"])
 @pytest.mark.parametrize("width,nhd", [(64, 2), (64, 1), (32, 2), (32, 1)])
-def test_ingp_field_bwd_relaunch_deterministic(dev, width, nhd, mma, mode):
+def test_ingp_field_bwd_relaunch_deterministic(dev, width, nhd, mma):
     """Guard for the field backward's hand-placed hazard wait states (inline-asm MFMAs and
     ReLU masks): 12 launches on the same inputs give bit-identical dL/denc and parameter
     gradients equal up to the atomic flush order (2e-5 of the largest: f32 sums of ~16 K
     contributions in launch-dependent order; measured 1.0e-6). A missing wait
     state shows as launch-to-launch differences first (r03: the ReLU-mask asm fed MFMA
     operands without its two wait states, and the W=32 two-hidden-layer dir weight
-    gradients differed from launch to launch by up to 3x their size)."""
+    gradients differed from launch to launch by up to 3x their size). The static check
+    of the same wait states is tests/test_mfma_hazards.py."""
     from atmonr_amd import _lib
 
     nb, R, n_per_ray = 4, 64, 256
@@ -899,24 +827,20 @@ def test_ingp_field_bwd_relaunch_deterministic(dev, width, nhd, mma, mode):
     dsig = torch.randn(M, device=dev, generator=g) * 1e-3
     ws_bytes = lib.anr_ingp_field_bwd_workspace_bytes(pb, db, code, M)
     ws = torch.empty(max(1, ws_bytes // 4), device=dev)
-    prev = lib.anr_ingp_field_force_bwd(mode)
-    try:
-        first = None
-        for _ in range(12):
-            d_enc = torch.empty(M, 32, device=dev)
-            g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
-            _lib.call("anr_ingp_field_bwd", pb, db, code, packed.data_ptr(), enc.data_ptr(), 32,
-                      dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
-                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(),
-                      ws.data_ptr() if ws_bytes else None, ws_bytes, s)
-            if first is None:
-                first = (d_enc, g_pos, g_dir)
-                continue
-            assert torch.equal(d_enc, first[0])
-            for a, b in ((g_pos, first[1]), (g_dir, first[2])):
-                assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item()
-    finally:
-        lib.anr_ingp_field_force_bwd(prev)
+    first = None
+    for _ in range(12):
+        d_enc = torch.empty(M, 32, device=dev)
+        g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
+        _lib.call("anr_ingp_field_bwd", pb, db, code, packed.data_ptr(), enc.data_ptr(), 32,
+                  dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
+                  d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(),
+                  ws.data_ptr() if ws_bytes else None, ws_bytes, s)
+        if first is None:
+            first = (d_enc, g_pos, g_dir)
+            continue
+        assert torch.equal(d_enc, first[0])
+        for a, b in ((g_pos, first[1]), (g_dir, first[2])):
+            assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item()
 
 
 @pytest.mark.gpu

@@ -1,9 +1,9 @@
 """Field backward alone at the bench shape (8,192 rays x 1,024 samples, W=64, 2 dir hidden
-layers, f16), for PMC passes and A/B timing of the backward generations
-(anr_ingp_field_force_bwd). Random weights, encodings and output gradients; prints the
-mean launch time over --iters launches (HIP events on the launch stream).
+layers, f16), for PMC passes and timing (the r03 A/B generations were removed in r04).
+Random weights, encodings and output gradients; prints the mean launch time over --iters
+launches (HIP events on the launch stream).
 
-usage: python tools/field_bwd_pmc.py --mode 1 [--iters 20] [--rays 8192]
+usage: python tools/field_bwd_pmc.py [--iters 20] [--rays 8192]
 """
 
 import argparse
@@ -19,7 +19,6 @@ from atmonr_amd import _lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rays", type=int, default=8192)
     ap.add_argument("--spr", type=int, default=1024)
@@ -48,7 +47,6 @@ def main():
     ws = torch.empty(max(1, wsb // 4), device=dev)
     d_enc = torch.empty(M, 32, device=dev)
     gp, gd = torch.zeros_like(pp), torch.zeros_like(pd)
-    prev = lib.anr_ingp_field_force_bwd(args.mode)
 
     def launch():
         _lib.call("anr_ingp_field_bwd", pb, db, code, packed.data_ptr(), enc.data_ptr(), 32,
@@ -66,8 +64,7 @@ def main():
         launch()
     e1.record()
     torch.cuda.synchronize()
-    lib.anr_ingp_field_force_bwd(prev)
-    print(json.dumps({"mode": args.mode, "mma": args.mma, "M": M,
+    print(json.dumps({"mma": args.mma, "M": M,
                       "ms_per_launch": e0.elapsed_time(e1) / args.iters}))
 
 

@@ -228,8 +228,8 @@ def field_fused(pipe) -> bool:
 @torch.no_grad()
 def field_density(pipe, pts: torch.Tensor) -> torch.Tensor:
     """sigma = relu(pos_mlp(pos_encoder(pts))[:, 0]) at hash-grid points (P, 3) through the
-    fused field kernels (hash forward, then anr_ingp_field_fwd, whose sigma output is
-    exactly this; the colour it also computes is discarded). The extract path of
+    fused kernels (hash forward, then anr_ingp_field_density: the pos MLP of
+    anr_ingp_field_fwd without the dir MLP, bit-identical sigma). The extract path of
     instant_ngp.py:208-247 and the occupancy grid's density function, for pipelines whose
     field is fused (the only path for bf16 networks)."""
     dev = pts.device
@@ -251,8 +251,7 @@ def field_density(pipe, pts: torch.Tensor) -> torch.Tensor:
                          dtype=torch.float16)
     call("anr_ingp_field_pack", pdesc, ddesc, mma, ptr(_lib.pack_source(pos_mod.params, mma)),
          ptr(_lib.pack_source(pipe.dir_mlp.params, mma)), ptr(packed), s, tag="field_pack")
-    dirs = torch.full((1, 3), 0.5, device=dev)  # one "ray" for all points: colour unused
-    color = torch.empty(P, pipe.dir_mlp.n_output_dims, device=dev, dtype=torch.float32)
-    call("anr_ingp_field_fwd", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc.stride(0),
-         ptr(dirs), P, P, ptr(sigma), ptr(color), color.stride(0), s, tag="field_fwd")
+    # the pos MLP only (anr_ingp_field_density): sigma bit-identical to the full field's
+    call("anr_ingp_field_density", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc.stride(0), P,
+         ptr(sigma), s, tag="field_density")
     return sigma

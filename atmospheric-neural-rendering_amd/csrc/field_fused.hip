@@ -704,6 +704,48 @@ __device__ __forceinline__ void st4g(_Float16* base, int ld, int mrow, int col, 
   *reinterpret_cast<h4*>(base + mrow * ld + col) = v;
 }
 
+// Density only: relu(pos_out[:, 0]) of tile_forward's pos MLP, the dir MLP (70 % of the
+// field's MFMA work) skipped -- the extract loop (instant_ngp.py:208-247: only the
+// extinction is read) and the occupancy grid's density. The same MFMA sequence as the
+// full forward's pos half, so sigma is bit-identical to anr_ingp_field_fwd's. Weights in
+// registers, one 16-row tile per wavefront step, the next tile's encodings in flight.
+template <int W, int NHD, bool BF>
+__global__ void __launch_bounds__(256) density_kernel(Args a) {
+  using N = Net<W, NHD>;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int waves = blockDim.x >> 6, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  h8 p0[N::NT], p1[N::KB];
+#pragma unroll
+  for (int i = 0; i < N::NT; ++i)
+    p0[i] = *reinterpret_cast<const h8*>(a.packed + N::oFP0 + i * N::F32 + lane * 8);
+#pragma unroll
+  for (int i = 0; i < N::KB; ++i)
+    p1[i] = *reinterpret_cast<const h8*>(a.packed + N::oFP1 + i * N::F32 + lane * 8);
+  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+  const int64_t n_tiles = (a.M + 15) / 16;
+  const int64_t tstride = static_cast<int64_t>(gridDim.x) * waves;
+  int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave;
+  auto load = [&](int64_t t) -> h8 {
+    const int64_t row = t * 16 + li;
+    if (row < a.M) return *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+    return h8{};
+  };
+  h8 nxe = tile < n_tiles ? load(tile) : h8{};
+  for (; tile < n_tiles; tile += tstride) {
+    const h8 xe = enc_in<BF>(nxe);
+    const int64_t tn = tile + tstride;
+    if (tn < n_tiles) nxe = load(tn);
+    h4 hp[N::NT];
+#pragma unroll
+    for (int nt = 0; nt < N::NT; ++nt) hp[nt] = relu_h4<BF>(mma32<BF>(p0[nt], xe, z4));
+    f4 po = z4;
+#pragma unroll
+    for (int kb = 0; kb < N::KB; ++kb) po = mma32<BF>(p1[kb], cat(hp[2 * kb], hp[2 * kb + 1]), po);
+    const int64_t row = tile * 16 + li;
+    if (g == 0 && row < a.M) a.sigma[row] = fmaxf(po[0], 0.0f);
+  }
+}
+
 // The f16 gradient scale's input for a wavefront with tiles [t_begin, t_end):
 // absmax_kernel's value (0 for a wavefront without rows).
 __device__ __forceinline__ float wave_grad_max(const Args& a, const float* wmax, int64_t w_id,
@@ -1307,6 +1349,14 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
 #undef ANR_FWD_LAUNCH
     return 0;
   }
+  if (op == 3) {
+    const int64_t tiles = (a.M + 15) / 16;
+    int64_t blocks = (tiles + waves - 1) / waves;
+    if (blocks > 256LL * 8) blocks = 256LL * 8;  // 8 blocks (32 waves) per CU, grid-stride
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((density_kernel<W, NHD, BF>), dim3(blocks), dim3(64 * waves), 0, st, a);
+    return 0;
+  }
   const bool fast = a.n_out == 4 && (a.d_color_stride & 3) == 0 && a.d_sigma != nullptr;
   if (a.loss_scale > 0.0f) {  // reference numerics: the register-transposed kernel, REF
     if constexpr (BF) {
@@ -1548,6 +1598,33 @@ extern "C" int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* d
                                   anr_stream_t stream) {
   return field_fwd(pos, dir, mma_dtype, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
                    sigma, color, color_stride, stream);
+}
+
+extern "C" int anr_ingp_field_density(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                      int32_t mma_dtype, const void* packed, const void* enc,
+                                      int64_t enc_stride, int64_t M, float* sigma,
+                                      anr_stream_t stream) {
+  const int v = variant(pos, dir);
+  ANR_CHECK_ARG(v != 0, "anr_ingp_field_density: unsupported pos/dir MLP pair");
+  ANR_CHECK_ARG(mma_ok(mma_dtype), "anr_ingp_field_density: mma_dtype must be ANR_F16 or ANR_BF16");
+  ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_density: bad M");
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(packed && enc && sigma, "anr_ingp_field_density: null pointer");
+  ANR_CHECK_ARG(enc_stride >= 32 && enc_stride % 8 == 0, "anr_ingp_field_density: bad stride");
+  ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(enc) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(packed) & 15) == 0,
+                "anr_ingp_field_density: enc/packed must be 16-byte aligned");
+  Args a{};
+  a.packed = static_cast<const _Float16*>(packed);
+  a.enc = static_cast<const _Float16*>(enc);
+  a.enc_stride = enc_stride;
+  a.M = M;
+  a.sigma = sigma;
+  ANR_CHECK_ARG(dispatch(v, mma_dtype == ANR_BF16, 3, a, nullptr, 0,
+                         reinterpret_cast<hipStream_t>(stream)) == 0,
+                "anr_ingp_field_density: no kernel for this shape");
+  ANR_CHECK_LAUNCH("anr_ingp_field_density");
+  return ANR_OK;
 }
 
 extern "C" int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir,

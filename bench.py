@@ -96,6 +96,8 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
                      "survey_bytes": M * (64 + 12 + 2 * grid.n_levels * 8 * 2 * 2)},
         # enc in, sigma + color out
         "field_fwd": {"bytes": M * (enc_b + 4 + 4 * nb), "flops": M * f_fwd},
+        # enc in, sigma out; the pos MLP only (extract / occupancy)
+        "field_density": {"bytes": M * (enc_b + 4), "flops": M * mlp_flops(pos)},
         # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; forward recompute + dX + dW
         "field_bwd": {"bytes": M * (enc_b + 4 * nb + 4 + 4 * grid.n_out), "flops": 3 * M * f_fwd},
     }

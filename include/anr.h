@@ -282,6 +282,13 @@ int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t
                        const void* packed, const void* enc, int64_t enc_stride,
                        const float* dirs, int64_t n_per_ray, int64_t M, float* sigma,
                        float* color, int64_t color_stride, anr_stream_t stream);
+/* Density only: sigma[r] = relu(pos_mlp(enc[r])[0]) (f32), bit-identical to
+ * anr_ingp_field_fwd's sigma, without the dir MLP -- the extract loop
+ * (scripts/extract.py:203-209 -> instant_ngp.py:208-247 reads only the extinction) and the
+ * occupancy grid. Same descriptors and packed weights as anr_ingp_field_fwd. */
+int anr_ingp_field_density(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,
+                           const void* packed, const void* enc, int64_t enc_stride, int64_t M,
+                           float* sigma, anr_stream_t stream);
 int anr_ingp_field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t mma_dtype,
                        const void* packed, const void* enc, int64_t enc_stride,
                        const float* dirs, int64_t n_per_ray, int64_t M, const float* d_sigma,

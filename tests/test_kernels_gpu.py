@@ -796,6 +796,39 @@ def test_ingp_field_unsupported_and_empty(dev):
 
 
 @pytest.mark.parametrize("mma", ["f16", "bf16"])
+@pytest.mark.parametrize("width,nhd,M", [(64, 2, 2654208), (64, 2, 77), (32, 1, 1000)])
+def test_ingp_field_density_equals_field_sigma(dev, width, nhd, M, mma):
+    """anr_ingp_field_density (the pos MLP only: extract / occupancy) returns exactly the
+    full field forward's sigma, at the extract batch (32,768 columns x 81 altitudes) and
+    ragged sizes."""
+    from atmonr_amd import _lib
+
+    nb = 4
+    code = _lib.BF16 if mma == "bf16" else _lib.F16
+    g = torch.Generator(device=dev).manual_seed(width + M)
+    lib = _lib.load()
+    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
+    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
+    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
+    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
+    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
+    s = _lib.stream(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", pb, db, code, pp.data_ptr(), pd.data_ptr(),
+              packed.data_ptr(), s)
+    dirs = torch.full((1, 3), 0.5, device=dev)
+    sig_full = torch.full((M,), -1.0, device=dev)
+    color = torch.empty(M, nb, device=dev)
+    _lib.call("anr_ingp_field_fwd", pb, db, code, packed.data_ptr(), enc.data_ptr(), 32,
+              dirs.data_ptr(), M, M, sig_full.data_ptr(), color.data_ptr(), nb, s)
+    sig = torch.full((M + 1,), -1.0, device=dev)
+    _lib.call("anr_ingp_field_density", pb, db, code, packed.data_ptr(), enc.data_ptr(), 32, M,
+              sig.data_ptr(), s)
+    assert torch.equal(sig[:M], sig_full)
+    assert sig[M].item() == -1.0 and (sig_full > 0).any()
+
+
+@pytest.mark.parametrize("mma", ["f16", "bf16"])
 @pytest.mark.parametrize("width,nhd", [(64, 2), (64, 1), (32, 2), (32, 1)])
 def test_ingp_field_bwd_relaunch_deterministic(dev, width, nhd, mma):
     """Guard for the field backward's hand-placed hazard wait states (inline-asm MFMAs and

@@ -256,7 +256,8 @@ _SIGNATURES = {
     ),
     "anr_composite_ref16_fwd": (
         c_int32,
-        [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, _P, _P, _P, _P, _P, _P],
+        [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, _P, _P, _P, _P, _P, _P,
+         _P, _P],
     ),
     "anr_composite_ref16_bwd": (
         c_int32,

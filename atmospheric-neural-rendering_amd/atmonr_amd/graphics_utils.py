@@ -82,7 +82,7 @@ class _CompositeRef16Fn(torch.autograd.Function):
     """render_with_surface with the reference's f16 numerics (anr_composite_ref16_*)."""
 
     @staticmethod
-    def forward(ctx, z, color, sigma, color_surf, z_scale: float, zero_rays):
+    def forward(ctx, z, color, sigma, color_surf, z_scale: float, zero_rays, want16: bool):
         B, N, C = color.shape
         if sigma.shape[2] != 1:
             raise ANRError("reference-numerics composite: one density channel (B, N, 1)")
@@ -96,16 +96,20 @@ class _CompositeRef16Fn(torch.autograd.Function):
         surf = torch.empty(B, C, device=dev, dtype=f16) if cs is not None else None
         weights = torch.empty(B, N, 1, device=dev, dtype=f16)
         alpha = torch.empty(B, N, 1, device=dev, dtype=f16)
+        c16 = torch.empty(B, N, C, device=dev, dtype=f16) if want16 else None
+        s16 = torch.empty(B, N, 1, device=dev, dtype=f16) if want16 else None
         call("anr_composite_ref16_fwd", ptr(zc), float(z_scale), ptr(color), ptr(sigma), ptr(cs),
              dtype_code(color.dtype), B, N, C, ptr(cm), ptr(atmo), ptr(surf), ptr(weights),
-             ptr(alpha), _lib.stream(dev), tag="composite_fwd")
+             ptr(alpha), ptr(c16), ptr(s16), _lib.stream(dev), tag="composite_fwd")
         ctx.save_for_backward(zc, color, sigma, cs)
         ctx.set_materialize_grads(False)
         ctx.z_scale = float(z_scale)
         ctx.zero_rays = zero_rays
-        if cs is None:
-            return cm, alpha, weights
-        return cm, alpha, weights, atmo, surf
+        outs = (cm, alpha, weights) if cs is None else (cm, alpha, weights, atmo, surf)
+        if want16:
+            ctx.mark_non_differentiable(c16, s16)
+            outs = outs + (c16, s16)
+        return outs
 
     @staticmethod
     def backward(ctx, g_cm, *unused):
@@ -125,11 +129,11 @@ class _CompositeRef16Fn(torch.autograd.Function):
              dtype_code(color.dtype), B, N, C, ptr(g_cm), ptr(d_color), ptr(d_sigma), ptr(d_cs),
              dtype_code(color.dtype), ptr(ctx.zero_rays), _lib.stream(dev),
              tag="composite_bwd")
-        return None, d_color, d_sigma, d_cs, None, None
+        return None, d_color, d_sigma, d_cs, None, None, None
 
 
 def render_with_surface_ref16(z_vals, color, sigma, color_surf, z_scale: float = 1.0,
-                              zero_rays: torch.Tensor | None = None):
+                              zero_rays: torch.Tensor | None = None, inputs_f16: bool = False):
     """graphics_utils.py:52-77 with the reference's Instant-NGP numerics: z cast to f16
     (after the f32 ``z_vals * z_scale``), every op rounded to f16, torch's CUDA
     accumulation (f16 cumprod / cumsum, f32 sum / prod), and torch's f16 autograd as the
@@ -137,11 +141,14 @@ def render_with_surface_ref16(z_vals, color, sigma, color_surf, z_scale: float =
     may be f32 (rounded to f16 on load, as a tcnn f16 output would be). Returns f16
     (color_map, alpha, weights, atmo, surf). ``zero_rays`` (int32 device tensor, optional)
     counts rays whose alpha rounded to exactly 1 in f16 (torch's zero-input backward
-    branch, not reproduced: those rays get zero gradients)."""
+    branch, not reproduced: those rays get zero gradients). ``inputs_f16``: also return
+    color and sigma rounded to f16 as the kernel reads them (tcnn's f16 outputs, which the
+    reference's forward returns), written by the same kernel."""
     _check(z_vals, color, sigma)
     if zero_rays is None:
         zero_rays = torch.zeros(1, dtype=torch.int32, device=color.device)
-    return _CompositeRef16Fn.apply(z_vals, color, sigma, color_surf, z_scale, zero_rays)
+    return _CompositeRef16Fn.apply(z_vals, color, sigma, color_surf, z_scale, zero_rays,
+                                   bool(inputs_f16))
 
 
 def _check(z_vals, color, sigma):

@@ -83,11 +83,10 @@ class InstantNGPPipeline(Pipeline):
                                             mlp_dtype == torch.float16 and occupancy is None):
             raise ValueError("numerics='reference' runs the fused f16 field (f16 modules, "
                              "no occupancy culling)")
-        # reference numerics: rays of the current step whose f16 alpha rounded to exactly 1
-        # (their gradients are zero, not torch's zero-input cumprod branch; ref16.hip),
-        # reset at every forward, and the total over the pipeline's life (zero_rays_total)
+        # reference numerics: rays whose f16 alpha rounded to exactly 1 (their gradients are
+        # zero, not torch's zero-input cumprod branch; ref16.hip), counted over the
+        # pipeline's life (zero_rays_total; the Trainer warns when it grows)
         self._zero_rays = None
-        self._zero_rays_sum = None
         self.surface_stream = os.environ.get("ANR_SURFACE_STREAM", "1") != "0"
         ingp = self.config["instant_ngp"]
         nb = self.config["num_bands"]
@@ -217,18 +216,14 @@ class InstantNGPPipeline(Pipeline):
         sigma = sigma.view(B, N, 1)
         color_surf = surf_branch()
         if self.numerics == "reference":
-            if self._zero_rays is None:
+            if self._zero_rays is None:  # counts over the pipeline's life (no per-step op)
                 self._zero_rays = torch.zeros(1, dtype=torch.int32, device=color.device)
-                self._zero_rays_sum = torch.zeros(1, dtype=torch.int64, device=color.device)
-            elif self.training:
-                self._zero_rays_sum += self._zero_rays  # the previous step's count
-                self._zero_rays.zero_()
-            color_map, _, weights, atmo, surf = render_with_surface_ref16(
+            # the kernel also writes tcnn's f16 colour / density outputs for the results
+            color_map, _, weights, atmo, surf, color, sigma = render_with_surface_ref16(
                 z_vals, color, sigma, color_surf, z_scale=self.scale / 1000,
-                zero_rays=self._zero_rays)
+                zero_rays=self._zero_rays, inputs_f16=True)
             if color_map.requires_grad:
                 color_map = _TcnnGradsAtBackwardEnd.apply(color_map, self)
-            color, sigma = color.half(), sigma.half()  # tcnn's f16 outputs in the results
         else:
             color_map, _, weights, atmo, surf = render_with_surface(
                 z_vals, color, sigma, color_surf, z_scale=self.scale / 1000)
@@ -281,7 +276,7 @@ class InstantNGPPipeline(Pipeline):
         dropped because an f16 alpha rounded to exactly 1 (synchronises; 0 otherwise)."""
         if self._zero_rays is None:
             return 0
-        return int((self._zero_rays_sum + self._zero_rays).item())
+        return int(self._zero_rays.item())
 
     def extract(self, pts: torch.Tensor) -> torch.Tensor:
         """Extinction at normalized scene points (P,3) (instant_ngp.py:208-247)."""

@@ -86,9 +86,16 @@ constexpr int kSeg = 256;  // samples per segment: 4 per lane
 // f16 multiply / add rounds exactly as h(a * b) / h(a + b) -- one dependent instruction
 // per step of the chain instead of three.
 struct FwdLds {
-  _Float16 q2[kSeg], alpha[kSeg], T[kSeg];
-  _Float16 t[kMaxC][kSeg];  // f16(f16(color) * w) per band, summed serially in f32
+  // padded past a segment's n samples with the chain's neutral elements, so the serial
+  // scans run in whole 8-sample (16-B) LDS vectors: q2 = 1 (cp * 1, pr * 1 exact), t = -0
+  // (x + -0 == x for every x, signed zeros included)
+  __attribute__((aligned(16))) _Float16 q2[kSeg];
+  __attribute__((aligned(16))) _Float16 alpha[kSeg];
+  __attribute__((aligned(16))) _Float16 T[kSeg];
+  __attribute__((aligned(16))) _Float16 t[kMaxC][kSeg];  // f16(f16(color) * w) per band
 };
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+constexpr float kNegZero = -0.0f;
 
 template <typename T>
 __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, float zs,
@@ -97,7 +104,8 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
                                                  const T* __restrict__ cs, int64_t B, int N,
                                                  int C, __half* cmap, __half* atmo_out,
                                                  __half* surf_out, __half* weights,
-                                                 __half* alpha_out) {
+                                                 __half* alpha_out, __half* color16,
+                                                 __half* sigma16) {
   __shared__ FwdLds L;
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
@@ -107,35 +115,56 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
   float acc = 0.0f;    // lane c < C: band c's sum over samples, f32 accumulator
   for (int s0 = 0; s0 < N; s0 += kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
-    for (int li = lane; li < n; li += 64) {
-      const Sample sm = sample(h(ld(sigma, b * N + s0 + li)), delta_ref(zr, zs, s0 + li, N));
-      L.q2[li] = static_cast<_Float16>(sm.q2);
-      L.alpha[li] = static_cast<_Float16>(sm.alpha);
-    }
-    __syncthreads();
-    if (lane == 0) {
-#pragma unroll 8
-      for (int li = 0; li < n; ++li) {
-        const _Float16 q2 = L.q2[li];
-        L.T[li] = cp;                                   // cumprod(...)[:, :-1]
-        cp = cp * q2;                                   // = h(cp * q2)
-        pr = pr * static_cast<float>(q2);               // (1 - alpha).prod   (:75)
+    const int nv = (n + 7) & ~7;
+    for (int li = lane; li < nv; li += 64) {
+      if (li < n) {
+        const float sg = h(ld(sigma, b * N + s0 + li));
+        if (sigma16) sigma16[b * N + s0 + li] = __float2half_rn(sg);
+        const Sample sm = sample(sg, delta_ref(zr, zs, s0 + li, N));
+        L.q2[li] = static_cast<_Float16>(sm.q2);
+        L.alpha[li] = static_cast<_Float16>(sm.alpha);
+      } else {
+        L.q2[li] = static_cast<_Float16>(1.0f);
       }
     }
     __syncthreads();
-    for (int li = lane; li < n; li += 64) {
-      const int64_t i = b * N + s0 + li;
-      const float al = static_cast<float>(L.alpha[li]);
-      const float w = h(al * static_cast<float>(L.T[li]));   // alpha * T    (:43-46)
-      for (int c = 0; c < C; ++c)
-        L.t[c][li] = static_cast<_Float16>(h(h(ld(color, i * C + c)) * w));  // (:48)
-      if (weights) weights[i] = __float2half_rn(w);
-      if (alpha_out) alpha_out[i] = __float2half_rn(al);
+    if (lane == 0) {
+      for (int l8 = 0; l8 < nv; l8 += 8) {
+        const h8v q = *reinterpret_cast<const h8v*>(&L.q2[l8]);
+        h8v tv;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          tv[k] = cp;                                   // cumprod(...)[:, :-1]
+          cp = cp * q[k];                               // = h(cp * q2)
+          pr = pr * static_cast<float>(q[k]);           // (1 - alpha).prod   (:75)
+        }
+        *reinterpret_cast<h8v*>(&L.T[l8]) = tv;
+      }
+    }
+    __syncthreads();
+    for (int li = lane; li < nv; li += 64) {
+      if (li < n) {
+        const int64_t i = b * N + s0 + li;
+        const float al = static_cast<float>(L.alpha[li]);
+        const float w = h(al * static_cast<float>(L.T[li]));   // alpha * T    (:43-46)
+        for (int c = 0; c < C; ++c) {
+          const float col = h(ld(color, i * C + c));
+          if (color16) color16[i * C + c] = __float2half_rn(col);
+          L.t[c][li] = static_cast<_Float16>(h(col * w));  // (:48)
+        }
+        if (weights) weights[i] = __float2half_rn(w);
+        if (alpha_out) alpha_out[i] = __float2half_rn(al);
+      } else {
+        for (int c = 0; c < C; ++c) L.t[c][li] = static_cast<_Float16>(kNegZero);
+      }
     }
     __syncthreads();
     if (lane < C) {
-#pragma unroll 8
-      for (int li = 0; li < n; ++li) acc = acc + static_cast<float>(L.t[lane][li]);
+      for (int l8 = 0; l8 < nv; l8 += 8) {
+        const h8v tv = *reinterpret_cast<const h8v*>(&L.t[lane][l8]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = acc + static_cast<float>(tv[k]);
+      }
     }
     __syncthreads();
   }
@@ -156,9 +185,10 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
 // phases as fwd_kernel: pass 1 replays the cumprod; pass 2 walks the segments from the
 // last, with the reversed cumsum (rc) as the one serial scan.
 struct BwdLds {
-  _Float16 q2[kSeg];
-  _Float16 u[kSeg];    // pass 1: T_k; pass 2: f16(T_k * dL/dT_k), the term k adds to rc
-  _Float16 rin[kSeg];  // rc before sample k's term: the cumprod backward at k + 1
+  // padded as FwdLds: q2 = 1, u = -0 past a segment's n samples
+  __attribute__((aligned(16))) _Float16 q2[kSeg];
+  __attribute__((aligned(16))) _Float16 u[kSeg];    // pass 1: T_k; pass 2: f16(T_k * dL/dT_k)
+  __attribute__((aligned(16))) _Float16 rin[kSeg];  // rc before sample k's term
 };
 
 template <typename T, typename G>
@@ -186,19 +216,28 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
   bool zero = false;
   for (int s0 = 0; s0 < N; s0 += kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
-    for (int li = lane; li < n; li += 64) {
-      const Sample sm = sample(h(ld(sigma, b * N + s0 + li)), delta_ref(zr, zs, s0 + li, N));
-      L.q2[li] = static_cast<_Float16>(sm.q2);
-      zero = zero || sm.q2 == 0.0f;
+    const int nv = (n + 7) & ~7;
+    for (int li = lane; li < nv; li += 64) {
+      if (li < n) {
+        const Sample sm = sample(h(ld(sigma, b * N + s0 + li)), delta_ref(zr, zs, s0 + li, N));
+        L.q2[li] = static_cast<_Float16>(sm.q2);
+        zero = zero || sm.q2 == 0.0f;
+      } else {
+        L.q2[li] = static_cast<_Float16>(1.0f);
+      }
     }
     __syncthreads();
     if (lane == 0) {
-#pragma unroll 8
-      for (int li = 0; li < n; ++li) {
-        const _Float16 q2 = L.q2[li];
-        L.u[li] = cp;  // T_i, staged for the coalesced scratch store below
-        cp = cp * q2;  // = h(cp * q2)
-        pr = pr * static_cast<float>(q2);
+      for (int l8 = 0; l8 < nv; l8 += 8) {
+        const h8v q = *reinterpret_cast<const h8v*>(&L.q2[l8]);
+        h8v tv;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          tv[k] = cp;  // T_i, staged for the coalesced scratch store below
+          cp = cp * q[k];  // = h(cp * q2)
+          pr = pr * static_cast<float>(q[k]);
+        }
+        *reinterpret_cast<h8v*>(&L.u[l8]) = tv;
       }
     }
     __syncthreads();
@@ -235,11 +274,15 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
   _Float16 rc = 0.0f;  // reversed cumsum at j = N: cp_N * 0 (lane 0)
   for (int s0 = ((N - 1) / kSeg) * kSeg; s0 >= 0; s0 -= kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
+    const int nv = (n + 7) & ~7;
     float e_[J], dl_[J], q2_[J], gab_[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int li = lane + 64 * j;
-      if (li >= n) continue;
+      if (li >= n) {
+        if (li < nv) L.u[li] = static_cast<_Float16>(kNegZero);
+        continue;
+      }
       const int64_t k = b * N + s0 + li;
       const float sig = h(ld(sigma, k));
       const Sample sm = sample(sig, delta_ref(zr, zs, s0 + li, N));
@@ -261,10 +304,15 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
     }
     __syncthreads();
     if (lane == 0) {
-#pragma unroll 8
-      for (int li = n - 1; li >= 0; --li) {
-        L.rin[li] = rc;
-        rc = rc + L.u[li];  // = h(rc + u)
+      for (int l8 = nv - 8; l8 >= 0; l8 -= 8) {
+        const h8v uv = *reinterpret_cast<const h8v*>(&L.u[l8]);
+        h8v rv;
+#pragma unroll
+        for (int k = 7; k >= 0; --k) {
+          rv[k] = rc;
+          rc = rc + uv[k];  // = h(rc + u)
+        }
+        *reinterpret_cast<h8v*>(&L.rin[l8]) = rv;
       }
     }
     __syncthreads();
@@ -418,7 +466,7 @@ extern "C" int anr_composite_ref16_fwd(const float* z, float z_scale, const void
                                        int32_t in_dtype, int64_t B, int32_t N, int32_t C,
                                        void* color_map, void* color_map_atmo,
                                        void* color_map_surf, void* weights, void* alpha,
-                                       anr_stream_t stream) {
+                                       void* color16, void* sigma16, anr_stream_t stream) {
   ANR_CHECK_ARG(z && color && sigma && color_map, "anr_composite_ref16_fwd: null argument");
   ANR_CHECK_ARG(B >= 0 && N >= 1 && C >= 1 && C <= ref16::kMaxC,
                 "anr_composite_ref16_fwd: bad shape B=%lld N=%d C=%d", (long long)B, N, C);
@@ -432,7 +480,8 @@ extern "C" int anr_composite_ref16_fwd(const float* z, float z_scale, const void
                      static_cast<const T*>(color_surf), B, N, C,                              \
                      static_cast<__half*>(color_map), static_cast<__half*>(color_map_atmo),  \
                      static_cast<__half*>(color_map_surf), static_cast<__half*>(weights),     \
-                     static_cast<__half*>(alpha))
+                     static_cast<__half*>(alpha), static_cast<__half*>(color16),              \
+                     static_cast<__half*>(sigma16))
   if (in_dtype == ANR_F16) ANR_R16F(__half); else ANR_R16F(float);
 #undef ANR_R16F
   ANR_CHECK_LAUNCH("anr_composite_ref16_fwd");

@@ -432,13 +432,15 @@ int anr_loss_fwd_bwd(int32_t loss_type, const void* color_map, int32_t pred_dtyp
  * Forward: z (B,N) f32 times z_scale in f32 then rounded to f16; color (B,N,C), sigma
  * (B,N,1), color_surf (B,C) (nullable) in in_dtype, rounded to f16 on load. Outputs f16:
  * color_map (B,C) [required], color_map_atmo, color_map_surf (B,C), weights, alpha
- * (B,N,1) (nullable). Replaces render_with_surface (graphics_utils.py:52-77) at
- * instant_ngp.py:187-192 in that mode. */
+ * (B,N,1) (nullable); color16 (B,N,C), sigma16 (B,N,1) (nullable): the f16-rounded
+ * inputs, i.e. tcnn's f16 outputs the reference's forward returns (instant_ngp.py:194-206).
+ * Replaces render_with_surface (graphics_utils.py:52-77) at instant_ngp.py:187-192 in that
+ * mode. */
 int anr_composite_ref16_fwd(const float* z, float z_scale, const void* color,
                             const void* sigma, const void* color_surf, int32_t in_dtype,
                             int64_t B, int32_t N, int32_t C, void* color_map,
                             void* color_map_atmo, void* color_map_surf, void* weights,
-                            void* alpha, anr_stream_t stream);
+                            void* alpha, void* color16, void* sigma16, anr_stream_t stream);
 /* Backward from dL/dcolor_map (B,C) f16 (torch's f16 autograd of the forward).
  * d_color (B,N,C), d_sigma (B,N,1) [required; also scratch for the cumprod outputs] and
  * d_color_surf (B,C) (nullable) in out_dtype, holding f16 values. zero_rays: one int32

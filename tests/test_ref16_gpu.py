@@ -111,3 +111,23 @@ def test_grad_quantize(dev):
     _lib.call("anr_grad_quantize_f16", t.data_ptr(), t.numel(), 128.0, _lib.stream(dev))
     want = (ref_f16.h(g * np.float32(128)).astype(np.float16) / np.float16(128)).astype(np.float32)
     assert np.array_equal(t.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("in_dtype", [torch.float16, torch.float32])
+def test_composite_ref16_writes_f16_inputs(dev, in_dtype):
+    """inputs_f16=True: the forward kernel also writes color and sigma as it reads them
+    (rounded to f16: tcnn's outputs, which the pipeline returns as color_fine / sigma_fine),
+    equal to torch's .half() of the inputs; the other outputs are unchanged."""
+    from atmonr_amd.graphics_utils import render_with_surface_ref16
+
+    z, sigma, color, cs, g = _case(24, 77, 0.5)
+    tz = torch.from_numpy(z).to(dev)
+    tc = torch.from_numpy(color).to(dev, in_dtype)
+    ts = torch.from_numpy(sigma).to(dev, in_dtype)
+    tcs = torch.from_numpy(cs).to(dev, in_dtype)
+    a = render_with_surface_ref16(tz, tc, ts, tcs, z_scale=100.0)
+    b = render_with_surface_ref16(tz, tc, ts, tcs, z_scale=100.0, inputs_f16=True)
+    assert len(b) == len(a) + 2
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert torch.equal(b[-2], tc.half()) and torch.equal(b[-1], ts.half())

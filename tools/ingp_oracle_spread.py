@@ -11,6 +11,7 @@ size of the host-vs-device libm differences of scene construction. Prints the PS
 0/8/16/32/64 iterations for every run (JSON with --out).
 
     python tools/ingp_oracle_spread.py [--runs 3] [--out profiles/r03_ingp_oracle_spread.json]
+    python tools/ingp_oracle_spread.py --samples 1024 --batch 64 --checkpoints 0,8,64
 """
 
 from __future__ import annotations
@@ -34,6 +35,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--iters", type=int, default=64)
+    ap.add_argument("--samples", type=int, default=64,
+                    help="samples per ray (the PSNR test also runs 1,024 at batch 64)")
+    ap.add_argument("--batch", type=int, default=ingp_psnr.BATCH)
+    ap.add_argument("--checkpoints", default="0,8,16,32,64")
     ap.add_argument("--out", default=None)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--semantics", default="reference")
@@ -47,7 +52,7 @@ def main():
     from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
 
     scene = SyntheticHARP2Dataset(n_views=8, img_size=16, device=torch.device("cpu"), seed=0)
-    cfg = ge._ingp_config(64)
+    cfg = ge._ingp_config(a.samples)
     p = InstantNGPPipeline(cfg, scene, dtype=torch.float16, fused=True, seed=5)
     state = p.state_dict()
     pp = scene.get_point_preprocessor("horizontal")
@@ -63,8 +68,9 @@ def main():
         else:
             runners[f"perturb_dirs{run}"] = ingp_psnr.OracleRunner(o, opt, perturb_dirs=run)
     t0 = time.time()
-    cps = tuple(c for c in ingp_psnr.CHECKPOINTS if c <= a.iters)
-    res = ingp_psnr.train_side_by_side(runners, scene, 64, checkpoints=cps)
+    cps = tuple(int(c) for c in a.checkpoints.split(",") if int(c) <= a.iters)
+    res = ingp_psnr.train_side_by_side(runners, scene, a.samples, checkpoints=cps,
+                                       batch=a.batch)
     for name, out in res.items():
         print(name, [round(r["psnr"], 4) for r in out], flush=True)
     print(f"{time.time() - t0:.0f}s")

@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r4_b1024_trace gpurun_out/r4_ref_trace
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "field" tests/test_ref16_gpu.py > gpurun_out/r4_quick_test.log 2>&1 || { tail -30 gpurun_out/r4_quick_test.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "field" tests/test_ref16_gpu.py tests/test_extract_gpu.py tests/test_graph_gpu.py > gpurun_out/r4_quick_test.log 2>&1 || { tail -30 gpurun_out/r4_quick_test.log; exit 1; }
 tail -2 gpurun_out/r4_quick_test.log
 timeout -k 10 120 python -u tools/ref16_bench.py > gpurun_out/r4_ref16_bench.log 2>&1 && cat gpurun_out/r4_ref16_bench.log || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4_b1024_trace -o run --output-format csv -- python3 bench.py --batch 1024 --graph on --numerics build --steps 20 --warmup 10 --no-cpu-baseline --no-alt-numerics --no-kernel-timer --spec-peaks > gpurun_out/r4_b1024_trace/trace.log 2>&1 || { tail -20 gpurun_out/r4_b1024_trace/trace.log; exit 1; }

@@ -69,10 +69,22 @@ class OracleRunner:
     is moved by one f16 ulp: one rounding of the reference's f16 backward done the other
     way."""
 
-    def __init__(self, oracle, opt_cfg, perturb_ray=None, perturb_dirs=None):
+    def __init__(self, oracle, opt_cfg, perturb_ray=None, perturb_dirs=None,
+                 master: str = "f64", grad_noise=None):
         self.o = oracle
         self.opt = oracle.optimizer(opt_cfg)
         self.perturb_ray = perturb_ray
+        # master="f32": parameters and AdamW moments rounded to f32 after every step, as
+        # the reference keeps them (tinycudann's f32 params, torch AdamW in f32; the oracle
+        # otherwise trains f64 masters)
+        self.master = master
+        # grad_noise=(eps, seed): every step, every parameter gradient times (1 + eps * n),
+        # n standard normal per element -- per-step arithmetic noise of the size the GPU's
+        # reference numerics differ from this oracle by (relative L2 ~3e-5, MFMA f32 vs
+        # f64 accumulation and the f16 rounding flips it causes)
+        self.grad_noise = grad_noise
+        self._noise_gen = (torch.Generator().manual_seed(int(grad_noise[1]))
+                           if grad_noise else None)
         # perturb_dirs=seed: every ray direction moved by one f32 ulp (sign per ray and
         # component from the seed) in training and rendering -- the size of the device-vs-
         # host f64 libm differences in scene construction (DESIGN §1 f2)
@@ -107,7 +119,24 @@ class OracleRunner:
         loss = self.o.loss(cb, res)
         self.opt.zero_grad()
         loss.backward()
+        if self.grad_noise:
+            with torch.no_grad():
+                for g in self.opt.param_groups:
+                    for p in g["params"]:
+                        if p.grad is not None:
+                            n = torch.randn(p.grad.shape, generator=self._noise_gen,
+                                            dtype=p.grad.dtype)
+                            p.grad.mul_(1 + self.grad_noise[0] * n)
         self.opt.step()
+        if self.master == "f32":
+            with torch.no_grad():
+                for g in self.opt.param_groups:
+                    for p in g["params"]:
+                        p.copy_(p.float().double())
+                        st = self.opt.state.get(p, {})
+                        for k in ("exp_avg", "exp_avg_sq"):
+                            if k in st:
+                                st[k].copy_(st[k].float().double())
         return loss.item()
 
     def render(self, b, u):

@@ -39,12 +39,17 @@ def main():
                     help="samples per ray (the PSNR test also runs 1,024 at batch 64)")
     ap.add_argument("--batch", type=int, default=ingp_psnr.BATCH)
     ap.add_argument("--checkpoints", default="0,8,16,32,64")
+    ap.add_argument("--noise", type=float, default=3e-5,
+                    help="--perturb gradnoise: relative per-step gradient noise")
     ap.add_argument("--out", default=None)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--semantics", default="reference")
     ap.add_argument("--ref-acc", default="cuda", help="cuda | cpu (oracle/ref_ingp.py)")
     ap.add_argument("--perturb", default="grad", help="grad: one f16 ulp of one ray's "
-                    "loss gradient at step 0; dirs: every ray direction by one f32 ulp")
+                    "loss gradient at step 0; dirs: every ray direction by one f32 ulp; "
+                    "f32master: one run with f32 parameters / AdamW moments (the "
+                    "reference's) beside the oracle's f64 masters; gradnoise: per-step "
+                    "relative gradient noise of --noise")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     import __graft_entry__ as ge
@@ -63,6 +68,12 @@ def main():
                                    half=True, semantics=a.semantics, ref_acc=a.ref_acc)
         if run < 0:
             runners["unperturbed"] = ingp_psnr.OracleRunner(o, opt)
+        elif a.perturb == "gradnoise":
+            runners[f"grad_noise{run}"] = ingp_psnr.OracleRunner(
+                o, opt, grad_noise=(a.noise, 100 + run))
+        elif a.perturb == "f32master":
+            if run == 0:
+                runners["f32_master"] = ingp_psnr.OracleRunner(o, opt, master="f32")
         elif a.perturb == "grad":
             runners[f"perturb_ray{run}"] = ingp_psnr.OracleRunner(o, opt, perturb_ray=run)
         else:

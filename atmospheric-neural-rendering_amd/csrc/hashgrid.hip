@@ -811,8 +811,10 @@ static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
 // but the grid still needs waves to hide the walk's latency. Measured (r04 sweep,
 // profiles/r04_hash_bwd_ksweep.md): at 1,024 rays x 1,024 samples K = 256 (4,096 waves)
 // takes 0.176 ms against 0.295 ms at the r03 rule's K = 32 and 0.244 ms at K = 512; at
-// 8,192 rays K = 256 / 512 / 1024 take 1.219 / 1.200 / 1.287 ms. Rule: 256 samples per
-// chunk down to 4,096 chunks, shorter below that; 512 once that still leaves >= 16,384.
+// 8,192 rays K = 256 / 512 / 1024 take 1.219 / 1.200 / 1.287 ms -- but in the bench step
+// K = 512 makes the STEP slower (3.227 / 3.228 ms at 256 vs 3.270 / 3.267 at 512, alternating
+// runs on one box, hash bwd 1.139 vs 1.129 ms: profiles/r04_hash_bwd_k_step_ab.log). Rule:
+// 256 samples per chunk down to 4,096 chunks, shorter below that.
 static int64_t env_k(const char* name) {
   const char* e = getenv(name);  // profiling override of the chunk length
   return e ? atoll(e) : 0;
@@ -820,7 +822,6 @@ static int64_t env_k(const char* name) {
 static int64_t pick_chunk_v2(int64_t M) {
   static const int64_t over = env_k("ANR_HASH_KB");
   if (over > 0) return over;
-  if (M >= 512LL * 16384) return 512;
   int64_t K = M / 4096;
   if (K < 1) K = 1;
   if (K > 256) K = 256;

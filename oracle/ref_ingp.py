@@ -96,13 +96,14 @@ class _TcnnCall(torch.autograd.Function):
     gradients rounded to f16 and unscaled."""
 
     @staticmethod
-    def forward(ctx, x, params, fn):
+    def forward(ctx, x, params, fn, sum_noise=None):
         with torch.enable_grad():
             x64 = x.detach().double().requires_grad_(x.requires_grad)
             p64 = params.detach().double().requires_grad_(True)
             y = fn(x64, p64)
         ctx.graph = (x64, p64, y)
         ctx.x_dtype = x.dtype
+        ctx.sum_noise = sum_noise
         return y.detach().half()
 
     @staticmethod
@@ -110,13 +111,23 @@ class _TcnnCall(torch.autograd.Function):
         x64, p64, y = ctx.graph
         gs = (g.float() * LOSS_SCALE).half().double()
         ins = (x64, p64) if x64.requires_grad else (p64,)
-        grads = torch.autograd.grad(y, ins, gs, allow_unused=True)
+        grads = torch.autograd.grad(y, ins, gs, allow_unused=True, retain_graph=True)
         gp = grads[-1]
+        if gp is not None and ctx.sum_noise is not None:
+            # SPREAD EXPERIMENT ONLY (tools/ingp_oracle_spread.py --perturb sumnoise): the
+            # parameter gradient as an f32 sum in another order would carry, per entry, an
+            # error of about u_f32 * sum|terms|; added here as seeded normal noise of that
+            # size (sum|terms| = the same backward with |upstream gradient|)
+            gen, factor = ctx.sum_noise
+            (ga,) = torch.autograd.grad(y, (p64,), gs.abs(), allow_unused=True)
+            if ga is not None:
+                n = torch.randn(gp.shape, generator=gen, dtype=gp.dtype)
+                gp = gp + n * factor * 2.0 ** -24 * ga
         gp = torch.zeros_like(p64) if gp is None else (gp.half() / LOSS_SCALE).double()
         gx = None
         if x64.requires_grad and grads[0] is not None:
             gx = (grads[0].half().double() / LOSS_SCALE).to(ctx.x_dtype)
-        return gx, gp, None
+        return gx, gp, None, None
 
 
 class RefInstantNGP:
@@ -228,7 +239,8 @@ class RefInstantNGP:
         pts = torch.cat([pts[..., :2], pts[..., 2:] / self.alt], dim=-1).float()
         ing = self.ingp
         pos_enc = _TcnnCall.apply(pts.reshape(B * N, 3), P["pos_encoder"],
-                                  self._grid_ref(self.pos_grid))
+                                  self._grid_ref(self.pos_grid),
+                                  getattr(self, "grid_sum_noise", None))
         pos_out = _TcnnCall.apply(pos_enc, P["pos_mlp"], lambda x, p: self._mlp_ref(
             x, p, 32, 16, ing["network"]))
         dirs = b["dir"][:, None].expand(B, N, 3).reshape(B * N, 3).float()

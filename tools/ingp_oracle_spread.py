@@ -49,7 +49,8 @@ def main():
                     "loss gradient at step 0; dirs: every ray direction by one f32 ulp; "
                     "f32master: one run with f32 parameters / AdamW moments (the "
                     "reference's) beside the oracle's f64 masters; gradnoise: per-step "
-                    "relative gradient noise of --noise")
+                    "relative gradient noise of --noise; sumnoise: the hash grid gradient "
+                    "with --noise x u_f32 x sum|terms| of f32 summation-order noise")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     import __graft_entry__ as ge
@@ -68,6 +69,9 @@ def main():
                                    half=True, semantics=a.semantics, ref_acc=a.ref_acc)
         if run < 0:
             runners["unperturbed"] = ingp_psnr.OracleRunner(o, opt)
+        elif a.perturb == "sumnoise":
+            runners[f"sum_noise{run}"] = ingp_psnr.OracleRunner(
+                o, opt, grad_noise=(a.noise, 200 + run, "sum"))
         elif a.perturb == "gradnoise":
             runners[f"grad_noise{run}"] = ingp_psnr.OracleRunner(
                 o, opt, grad_noise=(a.noise, 100 + run))

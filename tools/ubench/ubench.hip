@@ -150,6 +150,32 @@ __global__ void __launch_bounds__(256) xcc_map_kernel(uint32_t* __restrict__ out
   if (threadIdx.x == 0) out[blockIdx.x] = xcc & 0xFu;
 }
 
+// f16 subnormal handling (r04 reference-numerics drift probe): an MFMA operand, a
+// conversion and a native f16 multiply of the subnormal 2^-20
+typedef _Float16 ub_h8 __attribute__((ext_vector_type(8)));
+typedef float ub_f4 __attribute__((ext_vector_type(4)));
+__global__ void f16_denorm_kernel(float* out) {
+  const int l = threadIdx.x;
+  const float tiny = 9.5367431640625e-07f;  // 2^-20: an f16 subnormal
+  ub_h8 a = {}, b = {};
+  if (l == 0) {
+    a[0] = static_cast<_Float16>(tiny);
+    b[0] = static_cast<_Float16>(1.0f);
+  }
+  ub_f4 c = {0.0f, 0.0f, 0.0f, 0.0f};
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  volatile float vt = tiny;
+  const _Float16 h = static_cast<_Float16>(vt);
+  volatile _Float16 one = static_cast<_Float16>(1.0f);
+  const _Float16 m = h * one;
+  if (l == 0) {
+    out[0] = c[0];                        // MFMA: 2^-20 if f16 subnormal inputs are kept
+    out[1] = static_cast<float>(h);       // f32 -> f16 -> f32 conversion
+    out[2] = static_cast<float>(m);       // native f16 multiply
+    out[3] = tiny;
+  }
+}
+
 extern "C" {
 
 int ub_xcc_map(void* out, int blocks, int spin, void* stream) {
@@ -200,6 +226,11 @@ int ub_gather(const void* table, int64_t n_words, int iters, int blocks, uint32_
   if (n_words <= 0 || iters <= 0 || blocks <= 0) return 1;
   gather_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((const uint32_t*)table, n_words, iters,
                                                          seed, (uint32_t*)sink);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int ub_f16_denorm(float* out, void* stream) {
+  f16_denorm_kernel<<<1, 64, 0, (hipStream_t)stream>>>(out);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

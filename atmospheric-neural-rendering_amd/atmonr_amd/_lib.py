@@ -254,6 +254,7 @@ _SIGNATURES = {
         c_int32,
         [c_int32, _P, c_int32, c_int32, _P, _P, c_int64, c_float, c_float, _P, _P, _P, _P],
     ),
+    "anr_composite_ref16_set_rays": (c_int32, [c_int32]),
     "anr_composite_ref16_fwd": (
         c_int32,
         [_P, c_float, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, _P, _P, _P, _P, _P, _P,

@@ -19,12 +19,15 @@
 // of one lane over LDS.
 #pragma clang fp contract(off)
 
+#include <stdlib.h>
+
 #include "anr_common.h"
 
 namespace anr {
 namespace ref16 {
 
 constexpr int kMaxC = 8;
+constexpr int kSeg = 64;   // samples per ray and segment: one per lane
 
 __device__ __forceinline__ float h(float x) { return __half2float(__float2half_rn(x)); }
 
@@ -43,41 +46,84 @@ __device__ __forceinline__ float h64(double d) {
 template <typename T>
 __device__ __forceinline__ float ld(const T* p, int64_t i) { return to_f32<T>(p[i]); }
 
-// z_vals (f32) * scale -> f16 (graphics_utils.py:28)
-__device__ __forceinline__ float zh(const float* zr, float zs, int i) { return h(zr[i] * zs); }
-
 // delta_i = diff([0, (z_0 + z_1) / 2, ..., (z_{N-2} + z_{N-1}) / 2, z_{N-1}])_i in f16
-// (graphics_utils.py:31-35)
-__device__ __forceinline__ float delta_ref(const float* zr, float zs, int i, int N) {
-  const float zi = zh(zr, zs, i);
-  const float lo = i == 0 ? h(zi * 0.0f) : h(h(zh(zr, zs, i - 1) + zi) * 0.5f);
-  const float hi = i == N - 1 ? zi : h(h(zi + zh(zr, zs, i + 1)) * 0.5f);
+// (graphics_utils.py:31-35), z_vals (f32) * scale -> f16 first (graphics_utils.py:28); from
+// the raw f32 z values at i - 1, i, i + 1 (zm / zp unused at the ends)
+__device__ __forceinline__ float delta_z(float zm, float z0, float zp, float zs, int i, int N) {
+  const float zi = h(z0 * zs);
+  const float lo = i == 0 ? h(zi * 0.0f) : h(h(h(zm * zs) + zi) * 0.5f);
+  const float hi = i == N - 1 ? zi : h(h(zi + h(zp * zs)) * 0.5f);
   return h(hi - lo);
 }
+
+// A wavefront is the whole workgroup here: LDS written by one lane and read by another
+// needs only program order (LDS executes a wave's instructions in issue order) and a
+// compiler barrier. __syncthreads() would also wait for every global load and store in
+// flight (its workgroup-scope release), which is what kept these kernels latency-bound.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One segment's global inputs for the R rays of a wave, one sample per lane, loaded a
+// segment ahead so the loads are in flight during the current segment's scans.
+template <int R, bool COLOR, bool SIGMA>
+struct SegIn {
+  float zm[R], z0[R], zp[R], sg[R], col[R][kMaxC];
+
+  template <typename T>
+  __device__ __forceinline__ void fetch(const float* z, const T* sigma, const T* color,
+                                        int64_t b0, int nr, int s0, int N, int C, int lane) {
+    const int i = s0 + lane;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < nr && lane < N - s0 && lane < kSeg) {
+        const int64_t b = b0 + r;
+        const float* zr = z + b * N;
+        z0[r] = zr[i];
+        zm[r] = i > 0 ? zr[i - 1] : 0.0f;
+        zp[r] = i < N - 1 ? zr[i + 1] : 0.0f;
+        if (SIGMA) sg[r] = ld(sigma, b * N + i);
+        if (COLOR) {
+#pragma unroll
+          for (int c = 0; c < kMaxC; ++c)
+            if (c < C) col[r][c] = ld(color, (b * N + i) * C + c);
+        }
+      }
+    }
+  }
+};
 
 struct Sample {
   float delta, e, alpha, q2;  // q2 = 1 - alpha + 1e-10 (= om = 1 - alpha in f16)
 };
 
-__device__ __forceinline__ Sample sample(float sig, float dl) {
+__device__ __forceinline__ Sample from_e(float e, float dl) {
   Sample s;
   s.delta = dl;
-  const float x = h(-sig * dl);                       // -sigma * delta   (:38)
-  s.e = h64(exp(static_cast<double>(x)));             // exp
+  s.e = e;
   s.alpha = h(1.0f - s.e);                            // 1 - exp
   s.q2 = h(h(1.0f - s.alpha) + 1e-10f);               // 1 - alpha + 1e-10 (:45)
   return s;
 }
 
-// One wavefront per ray (block = 64 threads), samples in segments of kSeg. Each segment
-// splits into lane-parallel phases (the per-sample f16 ops: delta, exp, alpha, weights,
-// the colour products) and serial scans run by one lane over LDS (the f16 cumprod, the
-// f32 product and sums, the f16 reversed cumsum of the backward) -- exactly the
-// accumulations that have no parallel form rounding the same way. Every value is formed
-// by the same expression as in the one-thread-per-ray r03 kernels, so the outputs are
-// unchanged bit for bit; r03 ran everything serially from HBM, one ray per thread
-// (1.5 ms forward / 3.3 ms backward at 8,192 x 1,024, latency-bound).
-constexpr int kSeg = 256;  // samples per segment: 4 per lane
+__device__ __forceinline__ Sample sample(float sig, float dl) {
+  const float x = h(-sig * dl);                       // -sigma * delta   (:38)
+  return from_e(h64(exp(static_cast<double>(x))), dl);  // exp
+}
+
+// R rays per wavefront (block = 64 threads), samples in segments of kSeg = 64 per ray. A
+// segment splits into lane-parallel phases (the per-sample f16 ops: delta, exp, alpha,
+// weights, the colour products), run as R passes of one ray's 64 samples across the
+// lanes, and serial scans over LDS (the f16 cumprod, the f32 product and band sums, the
+// f16 reversed cumsum of the backward) -- exactly the accumulations that have no parallel
+// form rounding the same way. A scan runs on lane r for ray r (the band sums on lane
+// r * C + c), so one scan instruction advances R rays: at R = 1 (r04's first form, one
+// wave per ray) the scans left 63 of 64 lanes idle and were ~3/4 of the kernels' VALU
+// issue. Every value is formed by the same expression as in the one-thread-per-ray r03
+// kernels, so the outputs are unchanged bit for bit.
+constexpr int kPad = 72;   // LDS row stride in halves: 144 B = 36 banks, rows on distinct banks
 
 // Every staged value is an f16 value (the outputs of h()), so LDS holds them as f16. The
 // serial cumprod / reversed cumsum steps run in native f16 arithmetic: the f32 product of
@@ -85,19 +131,20 @@ constexpr int kSeg = 256;  // samples per segment: 4 per lane
 // below a quarter f16 ulp of the larger (both forms then return the larger), so one IEEE
 // f16 multiply / add rounds exactly as h(a * b) / h(a + b) -- one dependent instruction
 // per step of the chain instead of three.
-struct FwdLds {
+template <int R>
+struct __attribute__((aligned(16))) FwdLds {
   // padded past a segment's n samples with the chain's neutral elements, so the serial
   // scans run in whole 8-sample (16-B) LDS vectors: q2 = 1 (cp * 1, pr * 1 exact), t = -0
   // (x + -0 == x for every x, signed zeros included)
-  __attribute__((aligned(16))) _Float16 q2[kSeg];
-  __attribute__((aligned(16))) _Float16 alpha[kSeg];
-  __attribute__((aligned(16))) _Float16 T[kSeg];
-  __attribute__((aligned(16))) _Float16 t[kMaxC][kSeg];  // f16(f16(color) * w) per band
+  _Float16 q2[R][kPad];
+  _Float16 alpha[R][kPad];
+  _Float16 T[R][kPad];
+  _Float16 t[kMaxC][R][kPad];  // f16(f16(color) * w) per band
 };
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 constexpr float kNegZero = -0.0f;
 
-template <typename T>
+template <int R, typename T>
 __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, float zs,
                                                  const T* __restrict__ color,
                                                  const T* __restrict__ sigma,
@@ -106,31 +153,38 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
                                                  __half* surf_out, __half* weights,
                                                  __half* alpha_out, __half* color16,
                                                  __half* sigma16) {
-  __shared__ FwdLds L;
-  const int64_t b = blockIdx.x;
+  __shared__ FwdLds<R> L;
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int nr = B - b0 < R ? static_cast<int>(B - b0) : R;  // rays of this wave
   const int lane = threadIdx.x;
-  const float* zr = z + b * N;
-  _Float16 cp = 1.0f;  // cumprod output, f16 accumulator (cuda scan); lane 0
-  float pr = 1.0f;     // prod over samples, f32 accumulator; lane 0
-  float acc = 0.0f;    // lane c < C: band c's sum over samples, f32 accumulator
+  const int sr = lane / C, sc = lane - sr * C;  // band-sum lane: ray sr, band sc
+  _Float16 cp = 1.0f;  // lane r < nr: ray r's cumprod output, f16 accumulator (cuda scan)
+  float pr = 1.0f;     // lane r < nr: ray r's prod over samples, f32 accumulator
+  float acc = 0.0f;    // lane sr < nr: ray sr's band sc sum over samples, f32 accumulator
+  SegIn<R, true, true> nxt;
+  nxt.fetch(z, sigma, color, b0, nr, 0, N, C, lane);
   for (int s0 = 0; s0 < N; s0 += kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
     const int nv = (n + 7) & ~7;
-    for (int li = lane; li < nv; li += 64) {
-      if (li < n) {
-        const float sg = h(ld(sigma, b * N + s0 + li));
-        if (sigma16) sigma16[b * N + s0 + li] = __float2half_rn(sg);
-        const Sample sm = sample(sg, delta_ref(zr, zs, s0 + li, N));
-        L.q2[li] = static_cast<_Float16>(sm.q2);
-        L.alpha[li] = static_cast<_Float16>(sm.alpha);
-      } else {
-        L.q2[li] = static_cast<_Float16>(1.0f);
+    const SegIn<R, true, true> cur = nxt;
+    if (s0 + kSeg < N) nxt.fetch(z, sigma, color, b0, nr, s0 + kSeg, N, C, lane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < nr && lane < n) {
+        const int64_t b = b0 + r;
+        const float sg = h(cur.sg[r]);
+        if (sigma16) sigma16[b * N + s0 + lane] = __float2half_rn(sg);
+        const Sample sm = sample(sg, delta_z(cur.zm[r], cur.z0[r], cur.zp[r], zs, s0 + lane, N));
+        L.q2[r][lane] = static_cast<_Float16>(sm.q2);
+        L.alpha[r][lane] = static_cast<_Float16>(sm.alpha);
+      } else if (lane < nv) {
+        L.q2[r][lane] = static_cast<_Float16>(1.0f);
       }
     }
-    __syncthreads();
-    if (lane == 0) {
+    wave_sync();
+    if (lane < nr) {
       for (int l8 = 0; l8 < nv; l8 += 8) {
-        const h8v q = *reinterpret_cast<const h8v*>(&L.q2[l8]);
+        const h8v q = *reinterpret_cast<const h8v*>(&L.q2[lane][l8]);
         h8v tv;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -138,41 +192,45 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
           cp = cp * q[k];                               // = h(cp * q2)
           pr = pr * static_cast<float>(q[k]);           // (1 - alpha).prod   (:75)
         }
-        *reinterpret_cast<h8v*>(&L.T[l8]) = tv;
+        *reinterpret_cast<h8v*>(&L.T[lane][l8]) = tv;
       }
     }
-    __syncthreads();
-    for (int li = lane; li < nv; li += 64) {
-      if (li < n) {
-        const int64_t i = b * N + s0 + li;
-        const float al = static_cast<float>(L.alpha[li]);
-        const float w = h(al * static_cast<float>(L.T[li]));   // alpha * T    (:43-46)
-        for (int c = 0; c < C; ++c) {
-          const float col = h(ld(color, i * C + c));
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < nr && lane < n) {
+        const int64_t i = (b0 + r) * N + s0 + lane;
+        const float al = static_cast<float>(L.alpha[r][lane]);
+        const float w = h(al * static_cast<float>(L.T[r][lane]));   // alpha * T    (:43-46)
+#pragma unroll
+        for (int c = 0; c < kMaxC; ++c) {
+          if (c >= C) break;
+          const float col = h(cur.col[r][c]);
           if (color16) color16[i * C + c] = __float2half_rn(col);
-          L.t[c][li] = static_cast<_Float16>(h(col * w));  // (:48)
+          L.t[c][r][lane] = static_cast<_Float16>(h(col * w));  // (:48)
         }
         if (weights) weights[i] = __float2half_rn(w);
         if (alpha_out) alpha_out[i] = __float2half_rn(al);
-      } else {
-        for (int c = 0; c < C; ++c) L.t[c][li] = static_cast<_Float16>(kNegZero);
+      } else if (lane < nv) {
+        for (int c = 0; c < C; ++c) L.t[c][r][lane] = static_cast<_Float16>(kNegZero);
       }
     }
-    __syncthreads();
-    if (lane < C) {
+    wave_sync();
+    if (sr < nr) {
       for (int l8 = 0; l8 < nv; l8 += 8) {
-        const h8v tv = *reinterpret_cast<const h8v*>(&L.t[lane][l8]);
+        const h8v tv = *reinterpret_cast<const h8v*>(&L.t[sc][sr][l8]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc = acc + static_cast<float>(tv[k]);
       }
     }
-    __syncthreads();
+    wave_sync();
   }
-  pr = h(__shfl(pr, 0));
-  if (lane < C) {
-    const int c = lane;
+  const float prr = h(__shfl(pr, sr < R ? sr : 0));
+  if (sr < nr) {
+    const int64_t b = b0 + sr;
+    const int c = sc;
     const float atmo = h(acc);
-    const float surf = cs ? h(pr * h(ld(cs, b * C + c))) : 0.0f;
+    const float surf = cs ? h(prr * h(ld(cs, b * C + c))) : 0.0f;
     cmap[b * C + c] = __float2half_rn(cs ? h(atmo + surf) : atmo);          // (:76)
     if (atmo_out) atmo_out[b * C + c] = __float2half_rn(atmo);
     if (surf_out && cs) surf_out[b * C + c] = __float2half_rn(surf);
@@ -181,17 +239,22 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
 
 // Autograd of fwd_kernel for dL/dcolor_map (oracle/ref_f16.py render_bwd). d_sigma
 // (one value per sample) doubles as the scratch holding the forward's cumprod outputs T_i,
-// read back in the reverse pass before the gradient overwrites them. Same wave-per-ray
+// and d_color's first band as the one holding exp(-sigma * delta), both read back in the
+// reverse pass before the gradients overwrite them. Same R-rays-per-wave
 // phases as fwd_kernel: pass 1 replays the cumprod; pass 2 walks the segments from the
 // last, with the reversed cumsum (rc) as the one serial scan.
-struct BwdLds {
+template <int R>
+struct __attribute__((aligned(16))) BwdLds {
   // padded as FwdLds: q2 = 1, u = -0 past a segment's n samples
-  __attribute__((aligned(16))) _Float16 q2[kSeg];
-  __attribute__((aligned(16))) _Float16 u[kSeg];    // pass 1: T_k; pass 2: f16(T_k * dL/dT_k)
-  __attribute__((aligned(16))) _Float16 rin[kSeg];  // rc before sample k's term
+  _Float16 q2[R][kPad];
+  _Float16 u[R][kPad];    // pass 1: T_k; pass 2: f16(T_k * dL/dT_k)
+  _Float16 rin[R][kPad];  // rc before sample k's term
+  float g[R][kMaxC];      // dL/dcolor_map per ray and band
+  float g_pr[R];          // dL/d(surface product) per ray
+  float pr[R];            // the surface product per ray (f16 value)
 };
 
-template <typename T, typename G>
+template <int R, typename T, typename G>
 __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, float zs,
                                                  const T* __restrict__ color,
                                                  const T* __restrict__ sigma,
@@ -199,37 +262,48 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
                                                  int C, const __half* __restrict__ g_cm,
                                                  G* d_color, G* d_sigma, G* d_cs,
                                                  int* zero_rays) {
-  __shared__ BwdLds L;
-  constexpr int J = kSeg / 64;
-  const int64_t b = blockIdx.x;
+  __shared__ BwdLds<R> L;
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int nr = B - b0 < R ? static_cast<int>(B - b0) : R;
   const int lane = threadIdx.x;
-  const float* zr = z + b * N;
-  float g[kMaxC], csv[kMaxC];
-#pragma unroll
-  for (int c = 0; c < kMaxC; ++c) {
-    g[c] = c < C ? __half2float(g_cm[b * C + c]) : 0.0f;
-    csv[c] = (c < C && cs) ? h(ld(cs, b * C + c)) : 0.0f;
+  const int sr = lane / C, sc = lane - sr * C;
+  float gl = 0.0f;  // lane sr < nr: ray sr's band sc
+  if (sr < nr) {
+    gl = __half2float(g_cm[(b0 + sr) * C + sc]);
+    L.g[sr][sc] = gl;
   }
   // pass 1: the forward's cumprod outputs (scratch) and the surface product
   _Float16 cp = 1.0f;
   float pr = 1.0f;
-  bool zero = false;
+  uint32_t zmask = 0;  // bit r: ray r has an f16 alpha of 1 (uniform)
+  SegIn<R, false, true> nxt;
+  nxt.fetch(z, sigma, color, b0, nr, 0, N, C, lane);
   for (int s0 = 0; s0 < N; s0 += kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
     const int nv = (n + 7) & ~7;
-    for (int li = lane; li < nv; li += 64) {
-      if (li < n) {
-        const Sample sm = sample(h(ld(sigma, b * N + s0 + li)), delta_ref(zr, zs, s0 + li, N));
-        L.q2[li] = static_cast<_Float16>(sm.q2);
-        zero = zero || sm.q2 == 0.0f;
-      } else {
-        L.q2[li] = static_cast<_Float16>(1.0f);
+    const SegIn<R, false, true> cur = nxt;
+    if (s0 + kSeg < N) nxt.fetch(z, sigma, color, b0, nr, s0 + kSeg, N, C, lane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      bool zr = false;
+      if (r < nr && lane < n) {
+        const int64_t b = b0 + r;
+        const Sample sm = sample(h(cur.sg[r]),
+                                 delta_z(cur.zm[r], cur.z0[r], cur.zp[r], zs, s0 + lane, N));
+        L.q2[r][lane] = static_cast<_Float16>(sm.q2);
+        // exp(-sigma * delta) (an f16 value) parked in the sample's first d_color slot until
+        // pass 2 reads it back before writing that slot: one f64 exp per sample
+        d_color[(b * N + s0 + lane) * C] = static_cast<G>(sm.e);
+        zr = sm.q2 == 0.0f;
+      } else if (lane < nv) {
+        L.q2[r][lane] = static_cast<_Float16>(1.0f);
       }
+      if (__any(zr)) zmask |= 1u << r;
     }
-    __syncthreads();
-    if (lane == 0) {
+    wave_sync();
+    if (lane < nr) {
       for (int l8 = 0; l8 < nv; l8 += 8) {
-        const h8v q = *reinterpret_cast<const h8v*>(&L.q2[l8]);
+        const h8v q = *reinterpret_cast<const h8v*>(&L.q2[lane][l8]);
         h8v tv;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -237,102 +311,143 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
           cp = cp * q[k];  // = h(cp * q2)
           pr = pr * static_cast<float>(q[k]);
         }
-        *reinterpret_cast<h8v*>(&L.u[l8]) = tv;
+        *reinterpret_cast<h8v*>(&L.u[lane][l8]) = tv;
       }
     }
-    __syncthreads();
-    for (int li = lane; li < n; li += 64)
-      d_sigma[b * N + s0 + li] = static_cast<G>(static_cast<float>(L.u[li]));
-    __syncthreads();
-  }
-  pr = h(__shfl(pr, 0));
-  zero = __any(zero);
-  // surface term: surf = pr * cs -> dL/dpr (sum over bands), dL/dcs
-  float g_pr = 0.0f;
-  if (cs) {
+    wave_sync();
 #pragma unroll
-    for (int c = 0; c < kMaxC; ++c)
-      if (c < C) {
-        g_pr = g_pr + h(g[c] * csv[c]);
-        if (d_cs && lane == 0) d_cs[b * C + c] = static_cast<G>(h(g[c] * pr));
+    for (int r = 0; r < R; ++r)
+      if (r < nr && lane < n)
+        d_sigma[(b0 + r) * N + s0 + lane] = static_cast<G>(static_cast<float>(L.u[r][lane]));
+    wave_sync();
+  }
+  // surface term: surf = pr * cs -> dL/dpr (sum over bands), dL/dcs
+  const float prr = h(__shfl(pr, sr < R ? sr : 0));
+  if (lane < nr) L.pr[lane] = h(pr);
+  if (cs && sr < nr) {
+    if (d_cs) d_cs[(b0 + sr) * C + sc] = static_cast<G>(h(gl * prr));
+  }
+  if (lane < nr) {
+    float g_pr = 0.0f;
+    if (cs) {
+      for (int c = 0; c < C; ++c) {
+        const float csv = h(ld(cs, (b0 + lane) * C + c));
+        g_pr = g_pr + h(L.g[lane][c] * csv);
       }
-    g_pr = h(g_pr);
-  }
-  if (zero) {
-    // alpha rounded to 1 in f16 (sigma * delta > ~9): torch takes its zero-input backward
-    // branches (prod_safe_zeros_backward, cumprod's first-zero formula) -- not restated
-    // rounding for rounding; flagged to the caller, gradients of this ray set to 0
-    if (lane == 0) atomicAdd(zero_rays, 1);
-    for (int i = lane; i < N; i += 64) {
-      d_sigma[b * N + i] = static_cast<G>(0.0f);
-      for (int c = 0; c < C; ++c) d_color[(b * N + i) * C + c] = static_cast<G>(0.0f);
+      g_pr = h(g_pr);
     }
-    return;
+    L.g_pr[lane] = g_pr;
   }
+  // alpha rounded to 1 in f16 (sigma * delta > ~9): torch takes its zero-input backward
+  // branches (prod_safe_zeros_backward, cumprod's first-zero formula) -- not restated
+  // rounding for rounding; flagged to the caller, gradients of such a ray set to 0
+  if (zmask && lane == 0) atomicAdd(zero_rays, __popc(zmask));
+  wave_sync();
   // pass 2, reverse: reversed cumsum of cp * dL/dcp with an f16 accumulator
   // (cumprod_backward), then each sample's gradients in autograd's order
-  _Float16 rc = 0.0f;  // reversed cumsum at j = N: cp_N * 0 (lane 0)
+  _Float16 rc = 0.0f;  // lane r < nr: ray r's reversed cumsum, at j = N: cp_N * 0
+  // a segment's inputs, fetched one segment ahead: z, colour, and the parked T and exp
+  float zm_[R], z0_[R], zp_[R], ee_[R], tt_[R], col_[R][kMaxC];
+  auto fetch2 = [&](int s0) {
+    const int i = s0 + lane;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < nr && lane < N - s0) {
+        const int64_t k = (b0 + r) * N + i;
+        const float* zr = z + (b0 + r) * N;
+        z0_[r] = zr[i];
+        zm_[r] = i > 0 ? zr[i - 1] : 0.0f;
+        zp_[r] = i < N - 1 ? zr[i + 1] : 0.0f;
+        ee_[r] = static_cast<float>(d_color[k * C]);
+        tt_[r] = static_cast<float>(d_sigma[k]);
+#pragma unroll
+        for (int c = 0; c < kMaxC; ++c)
+          if (c < C) col_[r][c] = ld(color, k * C + c);
+      }
+    }
+  };
+  fetch2(((N - 1) / kSeg) * kSeg);
+  wave_sync();
   for (int s0 = ((N - 1) / kSeg) * kSeg; s0 >= 0; s0 -= kSeg) {
     const int n = N - s0 < kSeg ? N - s0 : kSeg;
     const int nv = (n + 7) & ~7;
-    float e_[J], dl_[J], q2_[J], gab_[J];
+    float czm[R], cz0[R], czp[R], cee[R], ctt[R], ccol[R][kMaxC];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int li = lane + 64 * j;
-      if (li >= n) {
-        if (li < nv) L.u[li] = static_cast<_Float16>(kNegZero);
+    for (int r = 0; r < R; ++r) {
+      czm[r] = zm_[r]; cz0[r] = z0_[r]; czp[r] = zp_[r]; cee[r] = ee_[r]; ctt[r] = tt_[r];
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) ccol[r][c] = col_[r][c];
+    }
+    if (s0 > 0) fetch2(s0 - kSeg);
+    float e_[R], dl_[R], q2_[R], gab_[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      e_[r] = dl_[r] = q2_[r] = gab_[r] = 0.0f;
+      if (!(r < nr && lane < n)) {
+        if (lane < nv) L.u[r][lane] = static_cast<_Float16>(kNegZero);
         continue;
       }
-      const int64_t k = b * N + s0 + li;
-      const float sig = h(ld(sigma, k));
-      const Sample sm = sample(sig, delta_ref(zr, zs, s0 + li, N));
-      const float Tk = static_cast<float>(d_sigma[k]);
+      const int64_t k = (b0 + r) * N + s0 + lane;
+      if (zmask & (1u << r)) {
+        L.u[r][lane] = static_cast<_Float16>(kNegZero);
+        for (int c = 0; c < C; ++c) d_color[k * C + c] = static_cast<G>(0.0f);
+        continue;
+      }
+      const Sample sm = from_e(cee[r], delta_z(czm[r], cz0[r], czp[r], zs, s0 + lane, N));
+      const float Tk = ctt[r];
       const float w = h(sm.alpha * Tk);
       float gw = 0.0f;
-      for (int c = 0; c < C; ++c) {
-        const float col = h(ld(color, k * C + c));
-        gw = gw + h(g[c] * col);                                  // sum_to_size over bands
-        d_color[k * C + c] = static_cast<G>(h(g[c] * w));         // color * w -> color
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) {
+        if (c >= C) break;
+        const float gc = L.g[r][c];
+        const float col = h(ccol[r][c]);
+        gw = gw + h(gc * col);                                    // sum_to_size over bands
+        d_color[k * C + c] = static_cast<G>(h(gc * w));           // color * w -> color
       }
       gw = h(gw);
-      gab_[j] = h(gw * Tk);                                       // alpha * T -> alpha
+      gab_[r] = h(gw * Tk);                                       // alpha * T -> alpha
       const float g_T = h(gw * sm.alpha);                         // -> T
-      L.u[li] = static_cast<_Float16>(h(Tk * g_T));               // cp_k * dL/dcp_k
-      e_[j] = sm.e;
-      dl_[j] = sm.delta;
-      q2_[j] = sm.q2;
+      L.u[r][lane] = static_cast<_Float16>(h(Tk * g_T));          // cp_k * dL/dcp_k
+      e_[r] = sm.e;
+      dl_[r] = sm.delta;
+      q2_[r] = sm.q2;
     }
-    __syncthreads();
-    if (lane == 0) {
+    wave_sync();
+    if (lane < nr) {
       for (int l8 = nv - 8; l8 >= 0; l8 -= 8) {
-        const h8v uv = *reinterpret_cast<const h8v*>(&L.u[l8]);
+        const h8v uv = *reinterpret_cast<const h8v*>(&L.u[lane][l8]);
         h8v rv;
 #pragma unroll
         for (int k = 7; k >= 0; --k) {
           rv[k] = rc;
           rc = rc + uv[k];  // = h(rc + u)
         }
-        *reinterpret_cast<h8v*>(&L.rin[l8]) = rv;
+        *reinterpret_cast<h8v*>(&L.rin[lane][l8]) = rv;
       }
     }
-    __syncthreads();
+    wave_sync();
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int li = lane + 64 * j;
-      if (li >= n) continue;
-      const float g_cpin = h(static_cast<float>(L.rin[li]) / q2_[j]);  // cumprod bwd at k+1
+    for (int r = 0; r < R; ++r) {
+      if (!(r < nr && lane < n)) continue;
+      const int64_t k = (b0 + r) * N + s0 + lane;
+      if (zmask & (1u << r)) {
+        d_sigma[k] = static_cast<G>(0.0f);
+        continue;
+      }
+      const float g_cpin = h(static_cast<float>(L.rin[r][lane]) / q2_[r]);  // cumprod bwd at k+1
       const float g_alpha_c = -g_cpin;                            // 1 - alpha + 1e-10
       float g_alpha;
       if (cs) {
-        const float g_om = h(g_pr * h(pr / q2_[j]));              // prod backward
-        g_alpha = h(h(-g_om + gab_[j]) + g_alpha_c);
+        const float g_om = h(L.g_pr[r] * h(L.pr[r] / q2_[r]));    // prod backward
+        g_alpha = h(h(-g_om + gab_[r]) + g_alpha_c);
       } else {
-        g_alpha = h(gab_[j] + g_alpha_c);
+        g_alpha = h(gab_[r] + g_alpha_c);
       }
-      const float g_x = h(-g_alpha * e_[j]);                      // 1 - exp(x)
-      d_sigma[b * N + s0 + li] = static_cast<G>(-h(g_x * dl_[j]));   // -sigma * delta
+      const float g_x = h(-g_alpha * e_[r]);                      // 1 - exp(x)
+      d_sigma[k] = static_cast<G>(-h(g_x * dl_[r]));              // -sigma * delta
     }
-    __syncthreads();
+    wave_sync();
   }
 }
 
@@ -456,10 +571,33 @@ __global__ void __launch_bounds__(256) quantize_kernel(float* __restrict__ g, in
     g[i] = h(h(g[i] * s) * inv_s);
 }
 
+// Rays per wavefront: 1 by default (ANR_REF16_R = 1 / 2 / 4 / 8, or
+// anr_composite_ref16_set_rays, overrides; r04 sweep in DESIGN.md §10), halved until the
+// band-sum lanes R * C fit the wave.
+static int g_rays = 0;
+static int rays_per_wave(int C) {
+  static const int env = [] {
+    const char* s = getenv("ANR_REF16_R");
+    const int v = s ? atoi(s) : 0;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 1;
+  }();
+  int R = g_rays ? g_rays : env;
+  while (R > 1 && R * C > 64) R /= 2;
+  return R;
+}
+
 }  // namespace ref16
 }  // namespace anr
 
 using namespace anr;
+
+extern "C" int anr_composite_ref16_set_rays(int32_t rays_per_wave) {
+  ANR_CHECK_ARG(rays_per_wave == 0 || rays_per_wave == 1 || rays_per_wave == 2 ||
+                    rays_per_wave == 4 || rays_per_wave == 8,
+                "anr_composite_ref16_set_rays: %d (0 = default, 1 / 2 / 4 / 8)", rays_per_wave);
+  ref16::g_rays = rays_per_wave;
+  return ANR_OK;
+}
 
 extern "C" int anr_composite_ref16_fwd(const float* z, float z_scale, const void* color,
                                        const void* sigma, const void* color_surf,
@@ -473,16 +611,25 @@ extern "C" int anr_composite_ref16_fwd(const float* z, float z_scale, const void
   ANR_CHECK_ARG(in_dtype == ANR_F16 || in_dtype == ANR_F32, "anr_composite_ref16_fwd: bad dtype");
   if (B == 0) return ANR_OK;
   ANR_CHECK_ARG(B < (1LL << 31), "anr_composite_ref16_fwd: B=%lld too large", (long long)B);
-  const dim3 grid(static_cast<unsigned>(B)), block(64);
-#define ANR_R16F(T)                                                                           \
-  hipLaunchKernelGGL(ref16::fwd_kernel<T>, grid, block, 0, as_stream(stream), z, z_scale,    \
+  const int R = ref16::rays_per_wave(C);
+#define ANR_R16F(RR, T)                                                                        \
+  hipLaunchKernelGGL((ref16::fwd_kernel<RR, T>), dim3(static_cast<unsigned>(ceil_div(B, RR))), \
+                     dim3(64), 0, as_stream(stream), z, z_scale,                               \
                      static_cast<const T*>(color), static_cast<const T*>(sigma),               \
                      static_cast<const T*>(color_surf), B, N, C,                              \
                      static_cast<__half*>(color_map), static_cast<__half*>(color_map_atmo),  \
                      static_cast<__half*>(color_map_surf), static_cast<__half*>(weights),     \
                      static_cast<__half*>(alpha), static_cast<__half*>(color16),              \
                      static_cast<__half*>(sigma16))
-  if (in_dtype == ANR_F16) ANR_R16F(__half); else ANR_R16F(float);
+#define ANR_R16F_T(T)                                                                         \
+  switch (R) {                                                                                \
+    case 1: ANR_R16F(1, T); break;                                                            \
+    case 2: ANR_R16F(2, T); break;                                                            \
+    case 4: ANR_R16F(4, T); break;                                                            \
+    default: ANR_R16F(8, T); break;                                                           \
+  }
+  if (in_dtype == ANR_F16) { ANR_R16F_T(__half) } else { ANR_R16F_T(float) }
+#undef ANR_R16F_T
 #undef ANR_R16F
   ANR_CHECK_LAUNCH("anr_composite_ref16_fwd");
   return ANR_OK;
@@ -505,18 +652,28 @@ extern "C" int anr_composite_ref16_bwd(const float* z, float z_scale, const void
                 "anr_composite_ref16_bwd: d_color_surf without color_surf");
   if (B == 0) return ANR_OK;
   ANR_CHECK_ARG(B < (1LL << 31), "anr_composite_ref16_bwd: B=%lld too large", (long long)B);
-  const dim3 grid(static_cast<unsigned>(B)), block(64);
-#define ANR_R16B(T, G)                                                                        \
-  hipLaunchKernelGGL((ref16::bwd_kernel<T, G>), grid, block, 0, as_stream(stream), z, z_scale, \
+  const int R = ref16::rays_per_wave(C);
+#define ANR_R16B(RR, T, G)                                                                     \
+  hipLaunchKernelGGL((ref16::bwd_kernel<RR, T, G>),                                           \
+                     dim3(static_cast<unsigned>(ceil_div(B, RR))), dim3(64), 0,               \
+                     as_stream(stream), z, z_scale,                                           \
                      static_cast<const T*>(color), static_cast<const T*>(sigma),               \
                      static_cast<const T*>(color_surf), B, N, C,                              \
                      static_cast<const __half*>(d_color_map), static_cast<G*>(d_color),       \
                      static_cast<G*>(d_sigma), static_cast<G*>(d_color_surf), zero_rays)
-  if (in_dtype == ANR_F16) {
-    if (out_dtype == ANR_F16) ANR_R16B(__half, __half); else ANR_R16B(__half, float);
-  } else {
-    if (out_dtype == ANR_F16) ANR_R16B(float, __half); else ANR_R16B(float, float);
+#define ANR_R16B_TG(T, G)                                                                     \
+  switch (R) {                                                                                \
+    case 1: ANR_R16B(1, T, G); break;                                                         \
+    case 2: ANR_R16B(2, T, G); break;                                                         \
+    case 4: ANR_R16B(4, T, G); break;                                                         \
+    default: ANR_R16B(8, T, G); break;                                                        \
   }
+  if (in_dtype == ANR_F16) {
+    if (out_dtype == ANR_F16) { ANR_R16B_TG(__half, __half) } else { ANR_R16B_TG(__half, float) }
+  } else {
+    if (out_dtype == ANR_F16) { ANR_R16B_TG(float, __half) } else { ANR_R16B_TG(float, float) }
+  }
+#undef ANR_R16B_TG
 #undef ANR_R16B
   ANR_CHECK_LAUNCH("anr_composite_ref16_bwd");
   return ANR_OK;

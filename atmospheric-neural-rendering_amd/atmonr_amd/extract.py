@@ -18,6 +18,7 @@ density MLP as the same kernels training uses; the host only slices index ranges
 
 from __future__ import annotations
 
+import inspect
 from pathlib import Path
 
 import numpy as np
@@ -71,15 +72,23 @@ class GridExtractDataset:
                  xyz=self.xyz.view(*self.shp, A, 3).cpu().numpy())
 
 
+def _extract(pipeline, pts, run_length):
+    """pipeline.extract with the column run length when the pipeline takes the hint (the
+    batches are whole columns of ``run_length`` altitudes)."""
+    if "run_length" in inspect.signature(pipeline.extract).parameters:
+        return pipeline.extract(pts, run_length=run_length)
+    return pipeline.extract(pts)
+
+
 def extract_volume(pipeline, dataset, extract_ds: GridExtractDataset, batch_size: int = 32768,
                    num_bands: int = 1) -> torch.Tensor:
     """scripts/extract.py:183-209: extinction (n_points, num_bands) in 1/m."""
-    loader = BatchLoader(extract_ds, batch_size=batch_size * extract_ds.sample_alt.shape[0],
-                         shuffle=False)
+    A = int(extract_ds.sample_alt.shape[0])
+    loader = BatchLoader(extract_ds, batch_size=batch_size * A, shuffle=False)
     sigma = torch.zeros((len(extract_ds), num_bands), device=extract_ds.device)
     offset = torch.as_tensor(dataset.offset, dtype=torch.float64, device=extract_ds.device)
     with torch.no_grad():
         for batch in loader:
             pts = (batch["xyz"] - offset) / dataset.scale
-            sigma[batch["idx"]] = pipeline.extract(pts).to(dtype=sigma.dtype) / dataset.scale
+            sigma[batch["idx"]] = _extract(pipeline, pts, A).to(dtype=sigma.dtype) / dataset.scale
     return sigma

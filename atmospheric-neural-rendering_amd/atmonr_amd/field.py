@@ -226,12 +226,14 @@ def field_fused(pipe) -> bool:
 
 
 @torch.no_grad()
-def field_density(pipe, pts: torch.Tensor) -> torch.Tensor:
+def field_density(pipe, pts: torch.Tensor, run_length: int = 0) -> torch.Tensor:
     """sigma = relu(pos_mlp(pos_encoder(pts))[:, 0]) at hash-grid points (P, 3) through the
     fused kernels (hash forward, then anr_ingp_field_density: the pos MLP of
     anr_ingp_field_fwd without the dir MLP, bit-identical sigma). The extract path of
     instant_ngp.py:208-247 and the occupancy grid's density function, for pipelines whose
-    field is fused (the only path for bf16 networks)."""
+    field is fused (the only path for bf16 networks). ``run_length``: the points come in
+    runs of that many spatial neighbours (an extract column's altitudes), which the
+    hash-grid walker's chunks then follow (anr_hashgrid_fwd_runs; same values)."""
     dev = pts.device
     s = _lib.stream(dev)
     P = pts.shape[0]
@@ -243,8 +245,9 @@ def field_density(pipe, pts: torch.Tensor) -> torch.Tensor:
     pts = pts.float().contiguous()
     t_hash = _lib.compute_copy(enc_mod.params, enc_mod.dtype)
     enc = torch.empty(P, grid.n_out, device=dev, dtype=torch.float16)
-    call("anr_hashgrid_fwd", ctypes.byref(grid.desc), ptr(pts), 3, P, ptr(t_hash),
-         dtype_code(t_hash.dtype), ptr(enc), _lib.F16, enc.stride(0), s, tag="hash_fwd")
+    call("anr_hashgrid_fwd_runs", ctypes.byref(grid.desc), ptr(pts), 3, P, int(run_length),
+         ptr(t_hash), dtype_code(t_hash.dtype), ptr(enc), _lib.F16, enc.stride(0), s,
+         tag="hash_fwd")
     mma = _mma_code(pipe)
     pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
     packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc), device=dev,

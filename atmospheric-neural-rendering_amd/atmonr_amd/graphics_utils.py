@@ -101,7 +101,14 @@ class _CompositeRef16Fn(torch.autograd.Function):
         call("anr_composite_ref16_fwd", ptr(zc), float(z_scale), ptr(color), ptr(sigma), ptr(cs),
              dtype_code(color.dtype), B, N, C, ptr(cm), ptr(atmo), ptr(surf), ptr(weights),
              ptr(alpha), ptr(c16), ptr(s16), _lib.stream(dev), tag="composite_fwd")
-        ctx.save_for_backward(zc, color, sigma, cs)
+        # the backward reads the inputs as f16 values either way: with the f16 copies at
+        # hand it reads those (half the bytes of f32 inputs) and still returns gradients in
+        # the inputs' dtype
+        ctx.out_dtype = color.dtype
+        if want16:
+            ctx.save_for_backward(zc, c16, s16, cs)
+        else:
+            ctx.save_for_backward(zc, color, sigma, cs)
         ctx.set_materialize_grads(False)
         ctx.z_scale = float(z_scale)
         ctx.zero_rays = zero_rays
@@ -122,13 +129,16 @@ class _CompositeRef16Fn(torch.autograd.Function):
         if g_cm is None:
             g_cm = torch.zeros(B, C, device=dev, dtype=torch.float16)
         g_cm = g_cm.to(torch.float16).contiguous()
-        d_color = torch.empty_like(color)
-        d_sigma = torch.empty_like(sigma)
-        d_cs = torch.empty_like(cs) if cs is not None and ctx.needs_input_grad[3] else None
+        od = ctx.out_dtype
+        d_color = torch.empty(color.shape, device=dev, dtype=od)
+        d_sigma = torch.empty(sigma.shape, device=dev, dtype=od)
+        d_cs = (torch.empty(cs.shape, device=dev, dtype=od)
+                if cs is not None and ctx.needs_input_grad[3] else None)
+        if cs is not None and cs.dtype != color.dtype:
+            cs = cs.to(color.dtype)
         call("anr_composite_ref16_bwd", ptr(zc), ctx.z_scale, ptr(color), ptr(sigma), ptr(cs),
              dtype_code(color.dtype), B, N, C, ptr(g_cm), ptr(d_color), ptr(d_sigma), ptr(d_cs),
-             dtype_code(color.dtype), ptr(ctx.zero_rays), _lib.stream(dev),
-             tag="composite_bwd")
+             dtype_code(od), ptr(ctx.zero_rays), _lib.stream(dev), tag="composite_bwd")
         return None, d_color, d_sigma, d_cs, None, None, None
 
 

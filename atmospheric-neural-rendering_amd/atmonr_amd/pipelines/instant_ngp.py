@@ -278,8 +278,11 @@ class InstantNGPPipeline(Pipeline):
             return 0
         return int(self._zero_rays.item())
 
-    def extract(self, pts: torch.Tensor) -> torch.Tensor:
-        """Extinction at normalized scene points (P,3) (instant_ngp.py:208-247)."""
+    def extract(self, pts: torch.Tensor, run_length: int = 0) -> torch.Tensor:
+        """Extinction at normalized scene points (P,3) (instant_ngp.py:208-247).
+        ``run_length`` (optional, not in the reference's signature): the points come in
+        runs of that many neighbours (an extract column), a hint for the hash-grid walker
+        that does not change the values."""
         if self.point_preprocessor:
             pts = preprocess_points(pts, self._prep_ngp)
         else:
@@ -289,7 +292,8 @@ class InstantNGPPipeline(Pipeline):
                 self.pos_encoder.dtype == torch.float16:
             # the fused field's sigma output IS relu(pos_out[:, 0]) (f32 accumulator);
             # returned in tcnn's output precision, as the reference's clip of pos_out
-            return field_density(self, pts).view(pts.shape[0], 1).to(self.pos_mlp.output_dtype)
+            return field_density(self, pts, run_length).view(pts.shape[0], 1).to(
+                self.pos_mlp.output_dtype)
         with torch.no_grad():
             pos_out = self.pos_mlp(self.pos_encoder(pts))
         return torch.clip(pos_out[..., : self.num_density_outputs].view(

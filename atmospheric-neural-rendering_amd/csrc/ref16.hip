@@ -142,6 +142,17 @@ struct __attribute__((aligned(16))) FwdLds {
   _Float16 t[kMaxC][R][kPad];  // f16(f16(color) * w) per band
 };
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+
+// f32 x f16 and f32 + f16 with one rounding, as the f32 ops on the converted f16 value:
+// fma(a, q, +0) = round(a * q) (a * q >= 0 here, so no -0 case) and fma(x, 1, acc) =
+// round(acc + x); one v_fma_mix_f32 each instead of a conversion and the op -- the serial
+// scans are most of these kernels' VALU issue
+__device__ __forceinline__ float mul_h(float a, _Float16 q) {
+  return __builtin_fmaf(a, static_cast<float>(q), 0.0f);
+}
+__device__ __forceinline__ float add_h(float acc, _Float16 x) {
+  return __builtin_fmaf(static_cast<float>(x), 1.0f, acc);
+}
 constexpr float kNegZero = -0.0f;
 
 template <int R, typename T>
@@ -190,7 +201,7 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
         for (int k = 0; k < 8; ++k) {
           tv[k] = cp;                                   // cumprod(...)[:, :-1]
           cp = cp * q[k];                               // = h(cp * q2)
-          pr = pr * static_cast<float>(q[k]);           // (1 - alpha).prod   (:75)
+          pr = mul_h(pr, q[k]);                         // (1 - alpha).prod   (:75)
         }
         *reinterpret_cast<h8v*>(&L.T[lane][l8]) = tv;
       }
@@ -220,7 +231,7 @@ __global__ void __launch_bounds__(64) fwd_kernel(const float* __restrict__ z, fl
       for (int l8 = 0; l8 < nv; l8 += 8) {
         const h8v tv = *reinterpret_cast<const h8v*>(&L.t[sc][sr][l8]);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc = acc + static_cast<float>(tv[k]);
+        for (int k = 0; k < 8; ++k) acc = add_h(acc, tv[k]);
       }
     }
     wave_sync();
@@ -309,7 +320,7 @@ __global__ void __launch_bounds__(64) bwd_kernel(const float* __restrict__ z, fl
         for (int k = 0; k < 8; ++k) {
           tv[k] = cp;  // T_i, staged for the coalesced scratch store below
           cp = cp * q[k];  // = h(cp * q2)
-          pr = pr * static_cast<float>(q[k]);
+          pr = mul_h(pr, q[k]);
         }
         *reinterpret_cast<h8v*>(&L.u[lane][l8]) = tv;
       }
@@ -571,7 +582,7 @@ __global__ void __launch_bounds__(256) quantize_kernel(float* __restrict__ g, in
     g[i] = h(h(g[i] * s) * inv_s);
 }
 
-// Rays per wavefront: 1 by default (ANR_REF16_R = 1 / 2 / 4 / 8, or
+// Rays per wavefront: 2 by default (ANR_REF16_R = 1 / 2 / 4 / 8, or
 // anr_composite_ref16_set_rays, overrides; r04 sweep in DESIGN.md §10), halved until the
 // band-sum lanes R * C fit the wave.
 static int g_rays = 0;
@@ -579,7 +590,7 @@ static int rays_per_wave(int C) {
   static const int env = [] {
     const char* s = getenv("ANR_REF16_R");
     const int v = s ? atoi(s) : 0;
-    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 1;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 2;
   }();
   int R = g_rays ? g_rays : env;
   while (R > 1 && R * C > 64) R /= 2;

@@ -320,7 +320,7 @@ def run_extract(args, ds, dev, rank, world, t_scene):
         b = batches[k[0] % len(batches)]
         k[0] += 1
         pts = (b["xyz"] - offset) / ds.scale
-        sigma[b["idx"]] = pipe.extract(pts).to(dtype=sigma.dtype) / ds.scale
+        sigma[b["idx"]] = pipe.extract(pts, run_length=A).to(dtype=sigma.dtype) / ds.scale
 
     for _ in range(args.warmup):
         step()

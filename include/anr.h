@@ -143,6 +143,14 @@ int anr_hashgrid_init(anr_hashgrid_desc* d, int32_t n_dims, int32_t n_levels,
 int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
                      int64_t M, const void* table, int32_t table_dtype, void* out,
                      int32_t out_dtype, int64_t out_stride, anr_stream_t stream);
+/* The same, for points that come in runs of run_length spatial neighbours (the altitudes
+ * of one extract column, scripts/extract.py:180-211; a ray's samples): the walker's
+ * chunks follow the runs (run_length <= 256; 0 = no hint, as anr_hashgrid_fwd). Outputs
+ * do not depend on it. */
+int anr_hashgrid_fwd_runs(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
+                          int64_t M, int64_t run_length, const void* table,
+                          int32_t table_dtype, void* out, int32_t out_dtype,
+                          int64_t out_stride, anr_stream_t stream);
 
 /* Kernel generation (test / A-B hook; process-wide; returns the previous mode, or
  * ANR_E_INVALID for an unknown mode; also ANR_HASHGRID_MODE): 0 = default (forward v6
@@ -427,7 +435,7 @@ int anr_loss_fwd_bwd(int32_t loss_type, const void* color_map, int32_t pred_dtyp
  * and tcnn's backward is loss-scaled f16 (tinycudann/modules.py, loss scale 128). These
  * entry points reproduce those roundings op by op (oracle/ref_f16.py is the restatement;
  * torch's CUDA accumulation: f16 accumulator in cumprod / cumsum, f32 in sum / prod).
- * R rays per wavefront (default 1): lane-parallel per-sample ops, the order-sensitive
+ * R rays per wavefront (default 2): lane-parallel per-sample ops, the order-sensitive
  * accumulations as serial scans, lane r for ray r.
  * ------------------------------------------------------------------------------------
  * Forward: z (B,N) f32 times z_scale in f32 then rounded to f16; color (B,N,C), sigma
@@ -438,7 +446,7 @@ int anr_loss_fwd_bwd(int32_t loss_type, const void* color_map, int32_t pred_dtyp
  * Replaces render_with_surface (graphics_utils.py:52-77) at instant_ngp.py:187-192 in that
  * mode. */
 /* Rays per wavefront of the two composite kernels: 1, 2, 4 or 8, or 0 for the default
- * (1, or ANR_REF16_R); halved while R * C > 64. Outputs do not depend on it. */
+ * (2, or ANR_REF16_R); halved while R * C > 64. Outputs do not depend on it. */
 int anr_composite_ref16_set_rays(int32_t rays_per_wave);
 int anr_composite_ref16_fwd(const float* z, float z_scale, const void* color,
                             const void* sigma, const void* color_surf, int32_t in_dtype,

@@ -90,13 +90,31 @@ class _RoundBoth(torch.autograd.Function):
         return g.half().double()
 
 
+class _GradNoise(torch.autograd.Function):
+    """SPREAD EXPERIMENT ONLY (tools/ingp_oracle_spread.py --perturb xnoise): identity
+    forward; backward multiplies the incoming gradient by (1 + factor * 2^-24 * n), n
+    standard normal -- an f32 accumulation's relative error, placed before the f16
+    rounding of the hidden-layer gradient that follows in autograd's order."""
+
+    @staticmethod
+    def forward(ctx, x, noise):
+        ctx.noise = noise
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        gen, factor = ctx.noise
+        return g * (1 + torch.randn(g.shape, generator=gen, dtype=g.dtype) * factor
+                    * 2.0 ** -24), None
+
+
 class _TcnnCall(torch.autograd.Function):
     """One tinycudann module call in reference semantics: f16 output; backward with the
     f16 gradient scaled by LOSS_SCALE, the f64 module graph run on it, parameter and input
     gradients rounded to f16 and unscaled."""
 
     @staticmethod
-    def forward(ctx, x, params, fn, sum_noise=None):
+    def forward(ctx, x, params, fn, sum_noise=None, x_noise=None):
         with torch.enable_grad():
             x64 = x.detach().double().requires_grad_(x.requires_grad)
             p64 = params.detach().double().requires_grad_(True)
@@ -104,6 +122,7 @@ class _TcnnCall(torch.autograd.Function):
         ctx.graph = (x64, p64, y)
         ctx.x_dtype = x.dtype
         ctx.sum_noise = sum_noise
+        ctx.x_noise = x_noise
         return y.detach().half()
 
     @staticmethod
@@ -126,8 +145,16 @@ class _TcnnCall(torch.autograd.Function):
         gp = torch.zeros_like(p64) if gp is None else (gp.half() / LOSS_SCALE).double()
         gx = None
         if x64.requires_grad and grads[0] is not None:
-            gx = (grads[0].half().double() / LOSS_SCALE).to(ctx.x_dtype)
-        return gx, gp, None, None
+            g0 = grads[0]
+            if ctx.x_noise is not None:
+                # SPREAD EXPERIMENT ONLY (--perturb xnoise): the input gradient as an f32
+                # dot product would carry a relative error of about u_f32 * sqrt(K); as
+                # seeded noise of that size before tcnn's f16 rounding
+                gen, factor = ctx.x_noise
+                g0 = g0 * (1 + torch.randn(g0.shape, generator=gen, dtype=g0.dtype)
+                           * factor * 2.0 ** -24)
+            gx = (g0.half().double() / LOSS_SCALE).to(ctx.x_dtype)
+        return gx, gp, None, None, None
 
 
 class RefInstantNGP:
@@ -223,6 +250,9 @@ class RefInstantNGP:
                 # f16 tile: relu, rounded value and gradient, mask on the stored f16
                 # activation (tcnn's ReLU backward)
                 h = ref_tcnn.ReluRound.apply(h, torch.float16, True)
+                xn = getattr(self, "mlp_x_noise", None)
+                if xn is not None:
+                    h = _GradNoise.apply(h, xn)
         return h[:, :n_out]
 
     def _grid_ref(self, cfg):
@@ -241,8 +271,9 @@ class RefInstantNGP:
         pos_enc = _TcnnCall.apply(pts.reshape(B * N, 3), P["pos_encoder"],
                                   self._grid_ref(self.pos_grid),
                                   getattr(self, "grid_sum_noise", None))
+        xn = getattr(self, "mlp_x_noise", None)
         pos_out = _TcnnCall.apply(pos_enc, P["pos_mlp"], lambda x, p: self._mlp_ref(
-            x, p, 32, 16, ing["network"]))
+            x, p, 32, 16, ing["network"]), None, xn)
         dirs = b["dir"][:, None].expand(B, N, 3).reshape(B * N, 3).float()
         # dir_encoder(cat[dirs, pos_out[:, 1:]]): the cat promotes to f32 (instant_ngp.py:
         # 165-169); SH2 | Identity, f16 output; the identity part passes the gradient
@@ -253,7 +284,7 @@ class RefInstantNGP:
             return torch.cat([sh, x[:, 3:]], dim=1) + 0.0 * p.sum()
         dir_enc = _TcnnCall.apply(x_dir, torch.zeros(1, dtype=torch.float64), dir_enc_fn)
         color = _TcnnCall.apply(dir_enc, P["dir_mlp"], lambda x, p: self._mlp_ref(
-            x, p, 19, self.nb, ing["rgb_network"]))
+            x, p, 19, self.nb, ing["rgb_network"]), None, xn)
         ps = ((b["origin"] + b["dir"] * b["len"][:, None] + 1) / 2).float()
         surf_in = torch.cat([ps[:, :2], b["dir"].float()], dim=1)
         surf_grid = self._grid_ref(self.surf_grid)
@@ -262,7 +293,7 @@ class RefInstantNGP:
             return torch.cat([surf_grid(x[:, :2], p), _sh2(x[:, 2:5])], dim=1)
         surf_enc = _TcnnCall.apply(surf_in, P["surf_encoder"], surf_enc_fn)
         color_surf = _TcnnCall.apply(surf_enc, P["surf_mlp"], lambda x, p: self._mlp_ref(
-            x, p, 36, self.nb, ing["surface_network"]))
+            x, p, 36, self.nb, ing["surface_network"]), None, xn)
         color = torch.relu(color.view(B, N, -1))
         color_surf = torch.relu(color_surf)
         sigma = torch.relu(pos_out[:, :1]).view(B, N, 1)

@@ -83,6 +83,12 @@ class OracleRunner:
         # reference numerics differ from this oracle by (relative L2 ~3e-5, MFMA f32 vs
         # f64 accumulation and the f16 rounding flips it causes)
         self.grad_noise = grad_noise
+        if grad_noise and len(grad_noise) > 2 and grad_noise[2] == "x":
+            # the MLPs' input gradients (dL/d encoding) carry f32-dot-product noise before
+            # tcnn's f16 rounding (oracle/ref_ingp.py _TcnnCall, spread experiments only)
+            self.o.mlp_x_noise = (torch.Generator().manual_seed(int(grad_noise[1])),
+                                  float(grad_noise[0]))
+            self.grad_noise = None
         if grad_noise and len(grad_noise) > 2 and grad_noise[2] == "sum":
             # the hash grid's parameter gradient carries f32-summation-order noise instead
             # (oracle/ref_ingp.py _TcnnCall, spread experiments only)

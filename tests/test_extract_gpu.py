@@ -117,6 +117,11 @@ def test_extract_full_batch_spot_rows(scene, dev):
     sigma = extract_volume(p, scene, grid, batch_size=32768)
     halves = extract_volume(p, scene, grid, batch_size=16384)
     assert torch.equal(sigma, halves)
+    # extract_volume hands the hash-grid walker the column length (81-point chunks); the
+    # default chunking of a plain extract() call gives the same values
+    off = torch.as_tensor(scene.offset, dtype=torch.float64, device=dev)
+    plain = p.extract((grid.xyz - off) / scene.scale).float() / scene.scale
+    assert torch.equal(sigma, plain)
     gen = torch.Generator().manual_seed(3)
     rows = torch.randint(0, len(grid), (4096,), generator=gen)
     pts = (grid.xyz[rows.to(dev)] - torch.as_tensor(scene.offset, dtype=torch.float64,

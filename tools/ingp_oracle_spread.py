@@ -69,6 +69,9 @@ def main():
                                    half=True, semantics=a.semantics, ref_acc=a.ref_acc)
         if run < 0:
             runners["unperturbed"] = ingp_psnr.OracleRunner(o, opt)
+        elif a.perturb == "xnoise":
+            runners[f"x_noise{run}"] = ingp_psnr.OracleRunner(
+                o, opt, grad_noise=(a.noise, 300 + run, "x"))
         elif a.perturb == "sumnoise":
             runners[f"sum_noise{run}"] = ingp_psnr.OracleRunner(
                 o, opt, grad_noise=(a.noise, 200 + run, "sum"))

@@ -1044,6 +1044,10 @@ extern "C" int anr_hashgrid_init(anr_hashgrid_desc* d, int32_t n_dims, int32_t n
       return ANR_E_UNSUPPORTED;                                                    \
   }
 
+extern "C" int64_t anr_hashgrid_bwd_chunk(int64_t M) {
+  return M > 0 ? anr::pick_chunk_v2(M) : 0;
+}
+
 extern "C" int anr_hashgrid_fwd_runs(const anr_hashgrid_desc* d, const float* x,
                                      int64_t x_stride, int64_t M, int64_t run_length,
                                      const void* table, int32_t table_dtype, void* out,

@@ -158,6 +158,9 @@ int anr_hashgrid_fwd_runs(const anr_hashgrid_desc* d, const float* x, int64_t x_
  * four-lanes-per-level), 1 = v1 both, 6 = forward v1 + backward v2 (the r01 default),
  * 7 = mode 0 with the backward's run-time-stride instantiation. */
 int anr_hashgrid_force_v1(int32_t mode);
+/* Samples per wavefront chunk the v2 backward uses for M points (host-side query: the
+ * request counter of tools/hash_requests.py replays the kernel's chunking with it). */
+int64_t anr_hashgrid_bwd_chunk(int64_t M);
 
 /* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)
  * f32, ACCUMULATED (caller zeroes). Duplicate corner updates inside a wavefront are

@@ -82,3 +82,19 @@ def test_mlp_param_counts():
         assert lib.anr_mlp_bwd_workspace_bytes(ctypes.byref(d), 8192) == 4 * nw * expect
         assert lib.anr_mlp_bwd_workspace_bytes(ctypes.byref(d), 1 << 17) == 0
         assert lib.anr_mlp_bwd_workspace_bytes(ctypes.byref(d), 0) == 0
+
+
+def test_hash_bwd_chunk_rule_is_queried_from_the_library():
+    """bench.py counts the hash backward's memory-side requests by replaying the kernel's
+    chunking (tools/hash_requests.py); the chunk length comes from the library itself,
+    so the count cannot drift from the kernel's rule (r04: a stale Python copy of the rule
+    once counted 512-sample chunks while the kernel ran 256)."""
+    from atmonr_amd import _lib
+    from tools import hash_requests
+
+    lib = _lib.load()
+    for M, K in [(0, 0), (1, 1), (4096, 1), (1024 * 1024, 256), (8192 * 1024, 256),
+                 (100_000, 24)]:
+        assert lib.anr_hashgrid_bwd_chunk(M) == K, M
+        if M:
+            assert hash_requests.bwd_chunk(M) == K

@@ -19,7 +19,6 @@ count is then measured from the run's own coordinates, not read from a stored PM
 
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -28,13 +27,11 @@ U32 = 0xFFFFFFFF
 
 
 def bwd_chunk(M: int) -> int:
-    """pick_chunk_v2 (csrc/hashgrid.hip): samples per wave of the v2 backward."""
-    over = int(os.environ.get("ANR_HASH_KB", "0") or 0)
-    if over > 0:
-        return over
-    if M >= 512 * 16384:
-        return 512
-    return max(1, min(256, M // 4096))
+    """pick_chunk_v2 (csrc/hashgrid.hip): samples per wave of the v2 backward, asked of
+    the library itself (anr_hashgrid_bwd_chunk, ANR_HASH_KB included)."""
+    from atmonr_amd import _lib
+
+    return int(_lib.load().anr_hashgrid_bwd_chunk(int(M)))
 
 
 def level_geometry(desc) -> list[dict]:

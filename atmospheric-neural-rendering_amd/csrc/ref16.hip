@@ -582,17 +582,18 @@ __global__ void __launch_bounds__(256) quantize_kernel(float* __restrict__ g, in
     g[i] = h(h(g[i] * s) * inv_s);
 }
 
-// Rays per wavefront: 2 by default (ANR_REF16_R = 1 / 2 / 4 / 8, or
-// anr_composite_ref16_set_rays, overrides; r04 sweep in DESIGN.md §10), halved until the
-// band-sum lanes R * C fit the wave.
+// Rays per wavefront: 2 from 8,192 rays up, 1 below (fewer rays leave SIMDs idle, and
+// then one ray per wave's extra waves beat the shared scans); ANR_REF16_R = 1 / 2 / 4 / 8
+// or anr_composite_ref16_set_rays overrides (r04 sweep in DESIGN.md §10). Halved until
+// the band-sum lanes R * C fit the wave.
 static int g_rays = 0;
-static int rays_per_wave(int C) {
+static int rays_per_wave(int C, int64_t B) {
   static const int env = [] {
     const char* s = getenv("ANR_REF16_R");
     const int v = s ? atoi(s) : 0;
-    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 2;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
   }();
-  int R = g_rays ? g_rays : env;
+  int R = g_rays ? g_rays : (env ? env : (B >= 8192 ? 2 : 1));
   while (R > 1 && R * C > 64) R /= 2;
   return R;
 }
@@ -622,7 +623,7 @@ extern "C" int anr_composite_ref16_fwd(const float* z, float z_scale, const void
   ANR_CHECK_ARG(in_dtype == ANR_F16 || in_dtype == ANR_F32, "anr_composite_ref16_fwd: bad dtype");
   if (B == 0) return ANR_OK;
   ANR_CHECK_ARG(B < (1LL << 31), "anr_composite_ref16_fwd: B=%lld too large", (long long)B);
-  const int R = ref16::rays_per_wave(C);
+  const int R = ref16::rays_per_wave(C, B);
 #define ANR_R16F(RR, T)                                                                        \
   hipLaunchKernelGGL((ref16::fwd_kernel<RR, T>), dim3(static_cast<unsigned>(ceil_div(B, RR))), \
                      dim3(64), 0, as_stream(stream), z, z_scale,                               \
@@ -663,7 +664,7 @@ extern "C" int anr_composite_ref16_bwd(const float* z, float z_scale, const void
                 "anr_composite_ref16_bwd: d_color_surf without color_surf");
   if (B == 0) return ANR_OK;
   ANR_CHECK_ARG(B < (1LL << 31), "anr_composite_ref16_bwd: B=%lld too large", (long long)B);
-  const int R = ref16::rays_per_wave(C);
+  const int R = ref16::rays_per_wave(C, B);
 #define ANR_R16B(RR, T, G)                                                                     \
   hipLaunchKernelGGL((ref16::bwd_kernel<RR, T, G>),                                           \
                      dim3(static_cast<unsigned>(ceil_div(B, RR))), dim3(64), 0,               \

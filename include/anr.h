@@ -438,7 +438,7 @@ int anr_loss_fwd_bwd(int32_t loss_type, const void* color_map, int32_t pred_dtyp
  * and tcnn's backward is loss-scaled f16 (tinycudann/modules.py, loss scale 128). These
  * entry points reproduce those roundings op by op (oracle/ref_f16.py is the restatement;
  * torch's CUDA accumulation: f16 accumulator in cumprod / cumsum, f32 in sum / prod).
- * R rays per wavefront (default 2): lane-parallel per-sample ops, the order-sensitive
+ * R rays per wavefront (2, or 1 below 8,192 rays): lane-parallel per-sample ops, the order-sensitive
  * accumulations as serial scans, lane r for ray r.
  * ------------------------------------------------------------------------------------
  * Forward: z (B,N) f32 times z_scale in f32 then rounded to f16; color (B,N,C), sigma
@@ -449,7 +449,8 @@ int anr_loss_fwd_bwd(int32_t loss_type, const void* color_map, int32_t pred_dtyp
  * Replaces render_with_surface (graphics_utils.py:52-77) at instant_ngp.py:187-192 in that
  * mode. */
 /* Rays per wavefront of the two composite kernels: 1, 2, 4 or 8, or 0 for the default
- * (2, or ANR_REF16_R); halved while R * C > 64. Outputs do not depend on it. */
+ * (2 from 8,192 rays up, else 1; or ANR_REF16_R); halved while R * C > 64. Outputs do
+ * not depend on it. */
 int anr_composite_ref16_set_rays(int32_t rays_per_wave);
 int anr_composite_ref16_fwd(const float* z, float z_scale, const void* color,
                             const void* sigma, const void* color_surf, int32_t in_dtype,

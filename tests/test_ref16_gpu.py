@@ -52,9 +52,9 @@ def rays_per_wave():
 @pytest.mark.parametrize("B,N,smax", [(64, 64, 2.0), (32, 1024, 2e-4), (32, 1024, 0.5),
                                       (40, 13, 1.0), (16, 256, 1e-3), (37, 200, 0.05)])
 @pytest.mark.parametrize("in_dtype", [torch.float16, torch.float32])
-@pytest.mark.parametrize("R", [0, 1, 8])
+@pytest.mark.parametrize("R", [0, 2, 8])
 def test_composite_ref16_bit_exact(dev, rays_per_wave, B, N, smax, in_dtype, R):
-    """Every output and gradient bit-exact; at the default R (2) and at 1 and 8 rays per
+    """Every output and gradient bit-exact; at the default R (1 at these ray counts) and at 2 and 8 rays per
     wavefront, with ray counts that leave the last wave part-filled (37, 13 samples)."""
     if R == 8 and in_dtype == torch.float32 and N == 1024:
         pytest.skip("covered by the f16 case")
@@ -88,7 +88,7 @@ def test_composite_ref16_flags_alpha_one(dev):
     assert zr > 0
 
 
-@pytest.mark.parametrize("R", [0, 1, 8])
+@pytest.mark.parametrize("R", [0, 2, 8])
 def test_composite_ref16_zero_rays_beside_normal_rays(dev, rays_per_wave, R):
     """Rays whose alpha rounds to 1 share wavefronts with ordinary rays: those get zero
     gradients and are counted; their neighbours stay bit-exact."""

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--numerics", default="reference")
     ap.add_argument("--samples", type=int, default=64)
     ap.add_argument("--rays", type=int, default=200)
+    ap.add_argument("--psnr-batch", action="store_true",
+                    help="the first batch and draws of tests/ingp_psnr.py instead")
     a = ap.parse_args()
     import __graft_entry__ as ge
     from atmonr_amd.batch_loader import BatchLoader
@@ -45,8 +47,13 @@ def main():
                                scene.max_i, half=True,
                                semantics="reference" if a.numerics == "reference" else "build")
     B, N = a.rays, a.samples
-    batch = next(iter(BatchLoader(scene, B, seed=1)))
-    u = torch.rand(B, N, generator=torch.Generator().manual_seed(2))
+    if a.psnr_batch:
+        from tests import ingp_psnr
+        batch = next(iter(BatchLoader(scene, B, seed=ingp_psnr.SEED_BATCH)))
+        u = torch.rand(B, N, generator=torch.Generator().manual_seed(ingp_psnr.SEED_U))
+    else:
+        batch = next(iter(BatchLoader(scene, B, seed=1)))
+        u = torch.rand(B, N, generator=torch.Generator().manual_seed(2))
     p.compute_loss(batch, p.forward(batch, u=u.to(dev))).backward()
     torch.cuda.synchronize()
     # oracle, with dL/dpos_enc retained
@@ -54,8 +61,8 @@ def main():
     captured = {}
     orig = ref_ingp._TcnnCall.apply
 
-    def spy(x, params, fn):
-        y = orig(x, params, fn)
+    def spy(x, params, fn, *rest):
+        y = orig(x, params, fn, *rest)
         if params is o.params["pos_encoder"]:
             y.retain_grad()
             captured["enc"] = y

@@ -663,7 +663,8 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v6_kernel(
 template <int D, typename TG, int XS, int DS>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride_rt, int64_t M,
-    int64_t K, const TG* __restrict__ dout, int64_t dout_stride_rt, float* __restrict__ dtable) {
+    int64_t K, const TG* __restrict__ dout, int64_t dout_stride_rt, float* __restrict__ dtable,
+    int skip_zero) {
   constexpr int NC = Corners<D>::NC;
   const int64_t x_stride = XS > 0 ? XS : x_stride_rt;
   const int64_t dout_stride = DS > 0 ? DS : dout_stride_rt;
@@ -719,7 +720,8 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
           // no test of acc != 0 here: a leaving corner's sum is zero only when its
           // weights were (samples exactly on the cell faces), and the per-corner test
           // cost more instructions than the rare zero requests it saves
-          const bool out = !keepx || LaneCorners<D>::leaves(c, dl);
+          const bool out = (!keepx || LaneCorners<D>::leaves(c, dl)) &&
+                           (!skip_zero || acc[c] != 0.0f);
           if (out && (HASH_EXP & 1) == 0)
             atomicAdd(grad + static_cast<int64_t>(idx[c]) * 2, acc[c]);
         }
@@ -925,6 +927,20 @@ static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
   return ANR_OK;
 }
 
+// Cell-move flushes skip corners whose sum is exactly zero (the chunk-end flush always
+// did). Under build numerics such sums are rare and the test is pure cost; under the
+// reference numerics most samples' f16 dL/denc underflow to zero (tcnn's x128 loss scale
+// rounds them away), and the memory-side request count at the chunk ends alone fell from
+// 20.8 M to 18.7 M per launch after the first step (profiles/r04_close PMC).
+// ANR_HASH_SKIP0 = 0 / 1 overrides (A/B hook); default on.
+static int bwd_skip_zero() {
+  static const int v = [] {
+    const char* e = getenv("ANR_HASH_SKIP0");
+    return e ? (atoi(e) != 0) : 1;
+  }();
+  return v;
+}
+
 template <int D, int F>
 static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const float* x,
                       int64_t x_stride, int64_t M, const void* dout, int32_t gdt,
@@ -938,7 +954,7 @@ static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 #define ANR_HG_BWD2(TG, XS_, DS_)                                                          \
   hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<D, TG, XS_, DS_>), grid, block, 0, s, G,        \
                      d->n_levels, x, x_stride, M, K, static_cast<const TG*>(dout),          \
-                     dout_stride, dtable)
+                     dout_stride, dtable, bwd_skip_zero())
     if (gdt == ANR_F16) {
       if (fixed) ANR_HG_BWD2(__half, 3, 32);
       else ANR_HG_BWD2(__half, 0, 0);

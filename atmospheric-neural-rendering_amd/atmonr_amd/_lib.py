@@ -166,6 +166,10 @@ _SIGNATURES = {
     ),
     "anr_hashgrid_force_v1": (c_int32, [c_int32]),
     "anr_hashgrid_bwd_chunk": (c_int64, [c_int64]),
+    "anr_hashgrid_bwd_count_requests": (
+        c_int32,
+        [POINTER(HashGridDesc), _P, c_int64, c_int64, _P, c_int32, c_int64, _P, _P, _P],
+    ),
     "anr_sh_fwd": (c_int32, [c_int32, _P, c_int64, c_int64, _P, c_int32, c_int64, _P]),
     "anr_sh_bwd": (
         c_int32,

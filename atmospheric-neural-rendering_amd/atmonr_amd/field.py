@@ -195,8 +195,11 @@ class IngpFieldFn(torch.autograd.Function):
                      ptr(d_color), d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos),
                      ptr(g_dir), ptr(ws), ws_bytes, s, tag="field_bwd")
         _done(direct_p, p_pos, direct_d, p_dir)  # MLP grads final: their all-reduce may start
-        if getattr(pipe, "_keep_d_enc", False):  # diagnostics (tools/ref16_field_diag.py)
+        if getattr(pipe, "_keep_d_enc", False):
+            # diagnostics (tools/ref16_field_diag.py) and bench.py's request count of this
+            # hash-grid backward (anr_hashgrid_bwd_count_requests on the same inputs)
             pipe._last_d_enc = d_enc
+            pipe._last_hash_bwd = (coords, d_enc, g_hash)
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
         _done(direct_h, p_hash)

@@ -660,11 +660,34 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v6_kernel(
 // every prefetch address is a per-batch scalar base plus immediate offsets: the walk
 // issues no per-sample address arithmetic (r01 spent ~25 scalar instructions per sample
 // on 64-bit clamped indices), and only a chunk's last two batches clamp.
-template <int D, typename TG, int XS, int DS>
+// Distinct 64-B segments among the active lanes' addresses: the memory-side requests one
+// wave-level float atomic instruction makes (MI355X_MICROARCH.md "Global float atomics").
+// Called in divergent code: the count is returned to the instruction's first active lane
+// only (0 elsewhere), so per-lane sums add every instruction exactly once.
+__device__ __forceinline__ uint32_t distinct_segments(bool active, uint64_t seg) {
+  uint64_t mask = __ballot(active);
+  const uint64_t execm = __ballot(true);
+  const bool first = (__lane_id() == __ffsll(static_cast<unsigned long long>(execm)) - 1);
+  uint32_t n = 0;
+  while (mask) {
+    const int l = __ffsll(static_cast<unsigned long long>(mask)) - 1;
+    const uint32_t lo = __shfl(static_cast<uint32_t>(seg), l);
+    const uint32_t hi = __shfl(static_cast<uint32_t>(seg >> 32), l);
+    const uint64_t s = (static_cast<uint64_t>(hi) << 32) | lo;
+    mask &= ~__ballot(active && seg == s);
+    ++n;
+  }
+  return first ? n : 0;
+}
+
+// COUNT: the request-count instrument (anr_hashgrid_bwd_count_requests): the same walk,
+// but every flush instruction adds its number of distinct 64-B segments to *count
+// instead of issuing the atomics (dtable is not written)
+template <int D, typename TG, int XS, int DS, bool COUNT = false>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride_rt, int64_t M,
     int64_t K, const TG* __restrict__ dout, int64_t dout_stride_rt, float* __restrict__ dtable,
-    int skip_zero) {
+    int skip_zero, unsigned long long* __restrict__ count = nullptr) {
   constexpr int NC = Corners<D>::NC;
   const int64_t x_stride = XS > 0 ? XS : x_stride_rt;
   const int64_t dout_stride = DS > 0 ? DS : dout_stride_rt;
@@ -691,6 +714,15 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
   float acc[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) acc[c] = 0.0f;
+  uint32_t n_req = 0;  // COUNT only (wave-uniform)
+  auto flush = [&](bool out, uint32_t e, float v) {
+    if constexpr (COUNT) {
+      n_req += distinct_segments(
+          out, reinterpret_cast<uintptr_t>(grad + static_cast<int64_t>(e) * 2) >> 6);
+    } else {
+      if (out && (HASH_EXP & 1) == 0) atomicAdd(grad + static_cast<int64_t>(e) * 2, v);
+    }
+  };
 
   auto step = [&](const float* xv, float gv) {
     float w[D];
@@ -722,8 +754,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
           // cost more instructions than the rare zero requests it saves
           const bool out = (!keepx || LaneCorners<D>::leaves(c, dl)) &&
                            (!skip_zero || acc[c] != 0.0f);
-          if (out && (HASH_EXP & 1) == 0)
-            atomicAdd(grad + static_cast<int64_t>(idx[c]) * 2, acc[c]);
+          flush(out, idx[c], acc[c]);
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[c] = nacc[c];
@@ -785,8 +816,11 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     uint32_t idx[NC];
     LaneCorners<D>::indices(li, cell, b, idx);
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (acc[c] != 0.0f) atomicAdd(grad + static_cast<int64_t>(idx[c]) * 2, acc[c]);
+    for (int c = 0; c < NC; ++c) flush(acc[c] != 0.0f, idx[c], acc[c]);
+  }
+  if constexpr (COUNT) {
+    // per lane (lanes above n_levels have returned; an instrument, not the hot path)
+    if (n_req) atomicAdd(count, static_cast<unsigned long long>(n_req));
   }
 }
 
@@ -1059,6 +1093,40 @@ extern "C" int anr_hashgrid_init(anr_hashgrid_desc* d, int32_t n_dims, int32_t n
                        d->n_features);                                             \
       return ANR_E_UNSUPPORTED;                                                    \
   }
+
+extern "C" int anr_hashgrid_bwd_count_requests(const anr_hashgrid_desc* d, const float* x,
+                                               int64_t x_stride, int64_t M, const void* dout,
+                                               int32_t dout_dtype, int64_t dout_stride,
+                                               const float* dtable, unsigned long long* count,
+                                               anr_stream_t stream) {
+  using namespace anr;
+  ANR_CHECK_ARG(d && x && dout && dtable && count, "anr_hashgrid_bwd_count_requests: null argument");
+  ANR_CHECK_ARG(M >= 0 && x_stride >= d->n_dims && dout_stride >= (int64_t)d->n_levels * d->n_features,
+                "anr_hashgrid_bwd_count_requests: bad shape/stride");
+  ANR_CHECK_ARG(dout_dtype == ANR_F16 || dout_dtype == ANR_F32,
+                "anr_hashgrid_bwd_count_requests: bad dtype");
+  if (!(d->n_dims == 3 && d->n_features == 2 && d->n_levels <= 16 && bwd_v2())) {
+    set_error("anr_hashgrid_bwd_count_requests: only the v2 backward (3-D, 2 features, <= 16 "
+              "levels) is instrumented");
+    return ANR_E_UNSUPPORTED;
+  }
+  if (M == 0) return ANR_OK;
+  GridLevels G;
+  ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_bwd_count_requests: descriptor not initialised");
+  const int64_t K = pick_chunk_v2(M);
+  const dim3 grid(static_cast<unsigned>(ceil_div(ceil_div(M, K), 4))), block(256);
+  float* tab = const_cast<float*>(dtable);  // not written in COUNT mode
+  if (dout_dtype == ANR_F16)
+    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, __half, 0, 0, true>), grid, block, 0,
+                       as_stream(stream), G, d->n_levels, x, x_stride, M, K,
+                       static_cast<const __half*>(dout), dout_stride, tab, bwd_skip_zero(), count);
+  else
+    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, float, 0, 0, true>), grid, block, 0,
+                       as_stream(stream), G, d->n_levels, x, x_stride, M, K,
+                       static_cast<const float*>(dout), dout_stride, tab, bwd_skip_zero(), count);
+  ANR_CHECK_LAUNCH("anr_hashgrid_bwd_count_requests");
+  return ANR_OK;
+}
 
 extern "C" int64_t anr_hashgrid_bwd_chunk(int64_t M) {
   return M > 0 ? anr::pick_chunk_v2(M) : 0;

@@ -20,6 +20,7 @@ oracle's CPU restatement of the configs/nerf.json train step (rank 0, N = 1 only
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -105,9 +106,9 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
     if requests is not None:
         out["hash_bwd"]["atomic_requests"] = float(requests)
         out["hash_bwd"]["atomic_requests_source"] = (
-            "counted in this run from the benched batch's coordinates (tools/hash_requests.py:"
-            " the kernel's chunking, cells and corner indexing, one 64-B request per distinct "
-            "segment of a wave instruction)")
+            "counted in this run: anr_hashgrid_bwd_count_requests replays the hash-grid "
+            "backward of one benched step over its own inputs (coordinates, dL/denc, gradient "
+            "buffer) and counts each flush instruction's distinct 64-B segments")
         if ent and ent.get("atomic_requests") and not stale:
             out["hash_bwd"]["atomic_requests_pmc"] = {
                 "requests": float(ent["atomic_requests"]), "source":
@@ -123,21 +124,42 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
     return out
 
 
-def count_hash_requests(job, n_samples: int) -> int | None:
-    """Memory-side atomic requests of the hash-grid backward on one batch of the benched
-    shape (the job's loader, stratified draws), counted from its coordinates
-    (tools/hash_requests.py). None when the pipeline has no fused hash grid."""
-    from atmonr_amd.samplers import sample_and_preprocess
-    from tools import hash_requests
+def count_hash_requests(job, n_samples: int) -> tuple[int, float] | None:
+    """Memory-side atomic requests of the hash-grid backward in one benched step: one
+    eager step of the job keeps the hash-grid backward's inputs (coordinates, dL/denc,
+    gradient buffer), and the instrumented launch anr_hashgrid_bwd_count_requests replays
+    that kernel over them, counting each flush instruction's distinct 64-B segments -- the
+    zero-sum corners the kernel skips included, so the count follows the numerics (most
+    f16 dL/denc underflow in reference numerics). Returns (requests, fraction of nonzero
+    dL/denc in that step: is the field alive?); None when the pipeline has no fused
+    v2-eligible hash grid."""
+    from atmonr_amd import _lib
 
     pipe = job.pipe
     grid = pipe.pos_encoder.hash_grids[0]
-    if grid.desc.n_features != 2 or grid.desc.n_levels > 16:
+    if grid.desc.n_features != 2 or grid.desc.n_levels > 16 or grid.desc.n_dims != 3:
         return None
-    with torch.no_grad():
-        batch = job.ds.__getbatch__(job.next_idx())
-        _, _, coords = sample_and_preprocess(batch, n_samples, pipe._prep_ngp)
-        return hash_requests.count(coords.view(-1, 3), grid.desc)
+    pipe._keep_d_enc = True
+    try:
+        job.eager_step()
+        coords, d_enc, g_hash = pipe._last_hash_bwd
+    except AttributeError:
+        return None
+    finally:
+        pipe._keep_d_enc = False
+    cnt = torch.zeros(1, dtype=torch.int64, device=coords.device)
+    _lib.call("anr_hashgrid_bwd_count_requests", ctypes.byref(grid.desc), coords.data_ptr(),
+              3, coords.shape[0], d_enc.data_ptr(), _lib.F32, d_enc.stride(0),
+              g_hash.data_ptr(), cnt.data_ptr(), _lib.stream(coords.device))
+    torch.cuda.synchronize()
+    if os.environ.get("ANR_BENCH_DEBUG"):
+        print(f"[count_hash_requests] M={coords.shape[0]} coords {tuple(coords.shape)} "
+              f"{coords.stride()} d_enc {tuple(d_enc.shape)} {d_enc.stride()} nonzero "
+              f"{(d_enc != 0).float().mean().item():.4f} g_hash {g_hash.numel()} "
+              f"count {int(cnt.item())}", file=sys.stderr, flush=True)
+    nz = (d_enc != 0).float().mean().item()
+    del pipe._last_hash_bwd, pipe._last_d_enc
+    return int(cnt.item()), nz
 
 
 def _roof(mdl: dict, avg_ms: float, peaks: dict, mfma_key: str) -> dict:
@@ -408,6 +430,29 @@ class _NullCtx:
 
     def __exit__(self, *exc):
         return False
+
+
+def warm_start(job, args, cfg, ds, dev, rank, world, rank_batch, shard) -> dict | None:
+    """Reference numerics start from a build-numerics warm-up. On the bench scene the first
+    AdamW step (lr 1e-2) kills the density ReLU at ~all samples in both numerics; the build
+    numerics' f32 gradients revive it by step ~8, the reference's f16 ones never do (40
+    steps: sigma > 0 at 0 % of samples, dL/denc all zero; profiles/r04_liveness_*.log), so a
+    reference-numerics step timed from a cold start would run a dead field whose backward
+    does no work. Its parameters are therefore taken from ``max(10, warmup)`` build-numerics
+    steps; from there the reference numerics keep the field alive (sigma > 0 at ~99 %,
+    12-33 % of dL/denc nonzero, the rest the reference's f16 underflow) and train on."""
+    if job.numerics != "reference":
+        return None
+    tmp = IngpJob(args, cfg, ds, dev, rank, world, rank_batch, "build", False, shard, None)
+    n = max(10, args.warmup)
+    for _ in range(n):
+        tmp.step()
+    with torch.no_grad():
+        job.pipe.load_state_dict(tmp.pipe.state_dict())
+    tmp.release()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return {"numerics": "build", "steps": n}
 
 
 class IngpJob:
@@ -695,6 +740,7 @@ def main():
     pipe, bucket, opt = job.pipe, job.bucket, job.opt
     sharded = job.sharded
     step = job.step
+    warm = warm_start(job, args, cfg, ds, dev, rank, world, rank_batch, shard)
 
     for _ in range(args.warmup):
         loss = step()
@@ -719,7 +765,8 @@ def main():
             pmc = {}
     pmc_sfx = (f"{args.variant}{'' if args.dtype == 'f16' else '-' + args.dtype}:"
                f"{rank_batch}x{args.samples}")
-    nreq = count_hash_requests(job, args.samples) if occ is None else None
+    req = count_hash_requests(job, args.samples) if occ is None else None
+    nreq = None if req is None else req[0]
     models = kernel_models(pipe, M, pmc, pmc_sfx, requests=nreq)
     kernels, dominant = {}, None
     if not args.no_kernel_timer:
@@ -798,8 +845,10 @@ def main():
         torch.cuda.empty_cache()
         ajob = IngpJob(args, cfg, ds, dev, rank, world, rank_batch, other, use_graph, shard,
                        None)
+        awarm = warm_start(ajob, args, cfg, ds, dev, rank, world, rank_batch, shard)
         for _ in range(args.warmup):
             ajob.step()
+        areq = count_hash_requests(ajob, args.samples)
         akern = ajob.profile(args.profile_steps, kernel_models(ajob.pipe, M), peaks, mfma_key)
         torch.cuda.synchronize()
         ta = time.perf_counter()
@@ -809,6 +858,8 @@ def main():
         ea = time.perf_counter() - ta
         alt = {"numerics": other, "value": round(rank_batch * args.steps / ea, 1),
                "ms_per_step": round(ea / args.steps * 1e3, 3), "graph": ajob.graphed,
+               "warm_start": awarm,
+               "d_enc_nonzero_frac": None if areq is None else round(areq[1], 4),
                "final_loss": round(float(aloss.item()), 6),
                "kernels": {k: {x: v[x] for x in ("avg_ms", "ms_per_step") if x in v}
                            for k, v in akern.items()}}
@@ -897,6 +948,8 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "numerics": numerics,
+            "warm_start": warm,
+            "d_enc_nonzero_frac": None if req is None else round(req[1], 4),
             "graph": job.graphed,
             "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} "
                     f"HARP2-shaped scene, {len(ds)} rays; random-init weights)",

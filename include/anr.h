@@ -161,6 +161,18 @@ int anr_hashgrid_force_v1(int32_t mode);
 /* Samples per wavefront chunk the v2 backward uses for M points (host-side query: the
  * request counter of tools/hash_requests.py replays the kernel's chunking with it). */
 int64_t anr_hashgrid_bwd_chunk(int64_t M);
+/* Request-count instrument of the v2 backward: the same launch geometry and walk over
+ * the same inputs as anr_hashgrid_bwd (dtable: the gradient buffer that launch would add
+ * to -- its addresses decide the 64-B segments; NOT written), adding to *count (one u64,
+ * device) the memory-side requests the real launch makes: per flush instruction, the
+ * distinct 64-B segments of its active lanes (zero-sum corners skipped as there).
+ * bench.py's hash-backward roofline counts its benched step this way. 3-D, 2 features,
+ * <= 16 levels; ANR_E_UNSUPPORTED otherwise. */
+int anr_hashgrid_bwd_count_requests(const anr_hashgrid_desc* d, const float* x,
+                                    int64_t x_stride, int64_t M, const void* dout,
+                                    int32_t dout_dtype, int64_t dout_stride,
+                                    const float* dtable, unsigned long long* count,
+                                    anr_stream_t stream);
 
 /* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)
  * f32, ACCUMULATED (caller zeroes). Duplicate corner updates inside a wavefront are

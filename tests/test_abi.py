@@ -85,10 +85,11 @@ def test_mlp_param_counts():
 
 
 def test_hash_bwd_chunk_rule_is_queried_from_the_library():
-    """bench.py counts the hash backward's memory-side requests by replaying the kernel's
-    chunking (tools/hash_requests.py); the chunk length comes from the library itself,
-    so the count cannot drift from the kernel's rule (r04: a stale Python copy of the rule
-    once counted 512-sample chunks while the kernel ran 256)."""
+    """tools/hash_requests.py replays the hash backward's chunking on the CPU (the
+    by-cause request analysis, and the reference for the GPU count instrument's test);
+    the chunk length comes from the library itself, so the replay cannot drift from the
+    kernel's rule (r04: a stale Python copy of the rule once counted 512-sample chunks
+    while the kernel ran 256)."""
     from atmonr_amd import _lib
     from tools import hash_requests
 

@@ -219,6 +219,53 @@ def test_hashgrid_bench_size_adjoint_and_spot_rows(dev, mode):
     assert abs(lhs - rhs) <= 1e-5 * scale, (lhs, rhs, scale)
 
 
+def test_hashgrid_bwd_request_count_instrument(dev):
+    """anr_hashgrid_bwd_count_requests (bench.py's in-run request count): with every
+    dL/denc nonzero it equals the CPU replay of the kernel's walk (tools/hash_requests.py,
+    itself checked against rocprofv3 TCC_EA0_ATOMIC_sum: 2.5086 vs 2.508 per sample);
+    all-zero gradients make no requests; zeroing the gradient of some samples can only
+    remove requests (the zero-sum corners the kernel skips); the gradient buffer is not
+    written. Ray-like coordinates at 64 rays x 1,024 samples (the PSNR test's shape)."""
+    from atmonr_amd import _lib
+    from tools import hash_requests
+
+    cfg = (3, 16, 16, 1.3819, 19)
+    d = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, 19)
+    M = 64 * 1024
+    gen = torch.Generator(device=dev).manual_seed(5)
+    # 64 straight rays of 1,024 samples inside the unit cube (no clamping: a sample exactly
+    # on a cell face gives a corner a zero weight, a zero sum the kernel skips and the CPU
+    # replay does not model)
+    o = 0.2 + 0.6 * torch.rand(64, 1, 3, device=dev, generator=gen)
+    dr = (torch.rand(64, 1, 3, device=dev, generator=gen) - 0.5) * 0.3
+    x = (o + dr * torch.linspace(0, 1, 1024, device=dev)[None, :, None]).reshape(M, 3).contiguous()
+    g = torch.randn(M, 32, device=dev, generator=gen)
+    g[g == 0] = 1.0
+    dtab = torch.zeros(d.n_params, device=dev)
+    s = _lib.stream(dev)
+
+    def count(grad):
+        c = torch.zeros(1, dtype=torch.int64, device=dev)
+        _lib.call("anr_hashgrid_bwd_count_requests", ctypes.byref(d), x.data_ptr(), 3, M,
+                  grad.data_ptr(), _lib.F32, grad.stride(0), dtab.data_ptr(), c.data_ptr(), s)
+        torch.cuda.synchronize()
+        return int(c.item())
+
+    full = count(g)
+    replay = hash_requests.count(x, d)
+    # the replay counts level by level; the instrument counts distinct segments over the
+    # whole wave instruction, so two levels' corners in one segment at a table-region
+    # border are one request there (and a rare sample exactly on a cell face gives a zero
+    # sum): measured 580,240 vs 580,261 (3.6e-5)
+    assert full <= replay and replay - full <= 1e-4 * replay, (full, replay)
+    assert count(torch.zeros_like(g)) == 0
+    gz = g.clone()
+    gz[torch.rand(M, device=dev, generator=gen) < 0.7] = 0.0
+    part = count(gz)
+    assert 0 < part < full
+    assert not dtab.any()
+
+
 def test_hashgrid_f16_table_and_strided_output(dev, hash_path):
     from atmonr_amd import _lib
 

@@ -106,7 +106,8 @@ class AdamTensor(Structure):
     """anr_adam_tensor (include/anr.h)."""
     _fields_ = [("params", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p),
                 ("exp_avg_sq", c_void_p), ("params_f16", c_void_p), ("n", c_int64),
-                ("lr", c_float), ("weight_decay", c_float), ("step", c_int64)]
+                ("lr", c_float), ("weight_decay", c_float), ("step", c_int64),
+                ("grad_quant", c_float)]
 
 
 ADAM_MAX_TENSORS = 16

@@ -24,6 +24,12 @@ from . import _lib
 from ._lib import call, ptr
 
 
+def _grad_quant(p) -> float:
+    """tinycudann's f16 gradient rounding deferred into this update (loss scale, or 0):
+    set on a parameter by InstantNGPPipeline.defer_grad_quantize."""
+    return float(getattr(p, "_anr_grad_quant", 0.0) or 0.0)
+
+
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=None,
                  decoupled: bool = True, zero_grad_in_step: bool = False,
@@ -118,7 +124,8 @@ class FusedAdam(torch.optim.Optimizer):
                     sh = None
                 ts.append(_lib.AdamTensor(ptr(p), ptr(p.grad), ptr(st["exp_avg"]),
                                           ptr(st["exp_avg_sq"]), ptr(sh), p.numel(),
-                                          float(group["lr"]), float(group["weight_decay"]), 0))
+                                          float(group["lr"]), float(group["weight_decay"]), 0,
+                                          _grad_quant(p)))
                 if sh is not None:
                     p._anr_shadow_ver = p._version
             arr = (_lib.AdamTensor * len(ts))(*ts)
@@ -187,7 +194,7 @@ class FusedAdam(torch.optim.Optimizer):
                 t = _lib.AdamTensor(ptr(p), ptr(p.grad), ptr(st["exp_avg"]),
                                     ptr(st["exp_avg_sq"]), ptr(sh), p.numel(),
                                     float(group["lr"]), float(group["weight_decay"]),
-                                    int(st["step"].item()))
+                                    int(st["step"].item()), _grad_quant(p))
                 batches.setdefault((p.device,) + key_hp, []).append(t)
                 if sh is not None:
                     p._anr_shadow_ver = p._version
@@ -198,6 +205,9 @@ class FusedAdam(torch.optim.Optimizer):
                      int(self.decoupled), int(self.zero_grad_in_step), _lib.stream(dev))
             else:
                 for t in ts:
+                    if t.grad_quant:
+                        raise _lib.ANRError("a deferred gradient quantisation needs "
+                                            "FusedAdam(multi_tensor=True)")
                     call("anr_adam_step", t.params, t.grad, t.exp_avg, t.exp_avg_sq,
                          t.params_f16, t.n, t.lr, b1, b2, eps, t.weight_decay,
                          int(self.decoupled), t.step, int(self.zero_grad_in_step),

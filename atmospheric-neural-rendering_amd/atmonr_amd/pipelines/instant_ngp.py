@@ -87,6 +87,7 @@ class InstantNGPPipeline(Pipeline):
         # zero, not torch's zero-input cumprod branch; ref16.hip), counted over the
         # pipeline's life (zero_rays_total; the Trainer warns when it grows)
         self._zero_rays = None
+        self._defer_quant = False  # defer_grad_quantize
         self.surface_stream = os.environ.get("ANR_SURFACE_STREAM", "1") != "0"
         ingp = self.config["instant_ngp"]
         nb = self.config["num_bands"]
@@ -123,6 +124,26 @@ class InstantNGPPipeline(Pipeline):
             occupancy = OccupancyGrid.from_config(occ_cfg, self.alt_compress,
                                                   getattr(dataset, "device", None))
         self.occupancy = occupancy
+
+    def defer_grad_quantize(self, optimizer) -> None:
+        """Reference numerics: leave tinycudann's f16 rounding of the parameter gradients,
+        f16(f16(g * 128) / 128), to ``optimizer`` -- a FusedAdam, which applies it as it
+        reads each gradient (anr_adam_tensor.grad_quant) -- instead of a separate pass over
+        every gradient at the end of backward (anr_grad_quantize_f16, ~0.03 ms per step at
+        the bench shape). The update is the same; ``param.grad`` between backward and the
+        step then holds the unrounded f32 sums, so code that reads or reduces gradients in
+        between (all-reduce, clipping, parity tests) must not defer. No-op in build
+        numerics."""
+        from ..optim import FusedAdam
+
+        if self.numerics != "reference":
+            return
+        if not isinstance(optimizer, FusedAdam) or not optimizer.multi_tensor:
+            raise ValueError("defer_grad_quantize needs a FusedAdam(multi_tensor=True)")
+        for m in self.modules():
+            if m.params.numel():
+                m.params._anr_grad_quant = float(self.loss_scale)
+        self._defer_quant = True
 
     # ------------------------------------------------------------------ module plumbing
     def modules(self):
@@ -348,6 +369,8 @@ class _TcnnGradsAtBackwardEnd(torch.autograd.Function):
         def quantize():
             main = torch.cuda.current_stream(dev)
             main.wait_stream(_lib.side_stream(dev))
+            if pipe._defer_quant:
+                return  # the optimizer rounds the gradients as it reads them
             grads = []
             for m in pipe.modules():
                 p = m.params

@@ -65,9 +65,16 @@ struct AdamTensors {
   int64_t n[ANR_ADAM_MAX_TENSORS];
   float wd[ANR_ADAM_MAX_TENSORS], decay[ANR_ADAM_MAX_TENSORS];
   float step_size[ANR_ADAM_MAX_TENSORS], bc2_sqrt[ANR_ADAM_MAX_TENSORS];
+  float gq[ANR_ADAM_MAX_TENSORS];  // grad_quant (0: none)
   int first[ANR_ADAM_MAX_TENSORS + 1];
   int count;
 };
+
+// anr_grad_quantize_f16's rounding on the update's read of g
+__device__ __forceinline__ float quant_f16(float g, float s) {
+  const float h1 = __half2float(__float2half_rn(g * s));
+  return __half2float(__float2half_rn(h1 * (1.0f / s)));
+}
 
 __global__ void __launch_bounds__(256) adam_multi_kernel(AdamTensors a, float b1, float b2,
                                                          float eps, int decoupled,
@@ -81,7 +88,7 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamTensors a, float b1
   __half* __restrict__ p16 = a.p16[t];
   const int64_t n = a.n[t];
   const float wd = a.wd[t], decay = a.decay[t], step_size = a.step_size[t],
-              bc2_sqrt = a.bc2_sqrt[t];
+              bc2_sqrt = a.bc2_sqrt[t], gq = a.gq[t];
   const float w1 = 1.0f - b1;
   const int64_t base = static_cast<int64_t>(static_cast<int>(blockIdx.x) - a.first[t]) * 1024;
 #pragma unroll
@@ -90,6 +97,7 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamTensors a, float b1
     if (i >= n) break;
     float pi = p[i];
     float gi = g[i];
+    if (gq != 0.0f) gi = quant_f16(gi, gq);
     if (wd != 0.0f) {
       if (decoupled)
         pi = pi * decay;
@@ -143,6 +151,7 @@ struct AdamTensorsDev {
   int64_t n[ANR_ADAM_MAX_TENSORS];
   float wd[ANR_ADAM_MAX_TENSORS];
   int idx[ANR_ADAM_MAX_TENSORS];  // the tensor's index in the caller's array (its scalars)
+  float gq[ANR_ADAM_MAX_TENSORS];  // grad_quant (0: none)
   int first[ANR_ADAM_MAX_TENSORS + 1];
   int count;
 };
@@ -159,7 +168,7 @@ __global__ void __launch_bounds__(256) adam_multi_dev_kernel(AdamTensorsDev a,
   float* __restrict__ v = a.v[t];
   __half* __restrict__ p16 = a.p16[t];
   const int64_t n = a.n[t];
-  const float wd = a.wd[t];
+  const float wd = a.wd[t], gq = a.gq[t];
   const float step_size = scal[3 * a.idx[t] + 0], bc2_sqrt = scal[3 * a.idx[t] + 1],
               decay = scal[3 * a.idx[t] + 2];
   const float w1 = 1.0f - b1;
@@ -170,6 +179,7 @@ __global__ void __launch_bounds__(256) adam_multi_dev_kernel(AdamTensorsDev a,
     if (i >= n) break;
     float pi = p[i];
     float gi = g[i];
+    if (gq != 0.0f) gi = quant_f16(gi, gq);
     if (wd != 0.0f) {
       if (decoupled)
         pi = pi * decay;
@@ -213,6 +223,8 @@ extern "C" int anr_adam_step_multi(const anr_adam_tensor* tensors, int32_t n_ten
     ANR_CHECK_ARG(d.n >= 0 && d.step >= 1, "anr_adam_step_multi: tensor %d: bad size/step", i);
     ANR_CHECK_ARG(d.n == 0 || (d.params && d.grad && d.exp_avg && d.exp_avg_sq),
                   "anr_adam_step_multi: tensor %d: null pointer", i);
+    ANR_CHECK_ARG(d.grad_quant >= 0.0f && d.grad_quant < 65504.0f,
+                  "anr_adam_step_multi: tensor %d: bad grad_quant", i);
   }
   int32_t t = 0;  // next tensor to place (empty tensors take no slot)
   while (t < n_tensors) {
@@ -233,6 +245,7 @@ extern "C" int anr_adam_step_multi(const anr_adam_tensor* tensors, int32_t n_ten
       a.p16[c] = static_cast<__half*>(d.params_f16);
       a.n[c] = d.n;
       a.wd[c] = d.weight_decay;
+      a.gq[c] = d.grad_quant;
       adam_scalars(d.lr, beta1, beta2, d.weight_decay, d.step, &a.step_size[c], &a.bc2_sqrt[c],
                    &a.decay[c]);
       a.first[c] = static_cast<int>(blocks);
@@ -284,6 +297,8 @@ extern "C" int anr_adam_step_multi_dev(const anr_adam_tensor* tensors, int32_t n
     ANR_CHECK_ARG(d.n >= 0, "anr_adam_step_multi_dev: tensor %d: bad size", i);
     ANR_CHECK_ARG(d.n == 0 || (d.params && d.grad && d.exp_avg && d.exp_avg_sq),
                   "anr_adam_step_multi_dev: tensor %d: null pointer", i);
+    ANR_CHECK_ARG(d.grad_quant >= 0.0f && d.grad_quant < 65504.0f,
+                  "anr_adam_step_multi_dev: tensor %d: bad grad_quant", i);
   }
   AdamWd wd;
   memset(&wd, 0, sizeof(wd));
@@ -307,6 +322,7 @@ extern "C" int anr_adam_step_multi_dev(const anr_adam_tensor* tensors, int32_t n
       a.p16[c] = static_cast<__half*>(d.params_f16);
       a.n[c] = d.n;
       a.wd[c] = d.weight_decay;
+      a.gq[c] = d.grad_quant;
       a.idx[c] = t;
       a.first[c] = static_cast<int>(blocks);
       blocks += ceil_div(d.n, 1024);

@@ -491,6 +491,10 @@ class IngpJob:
                               eps=opt_cfg["eps"], gather=shard)
         elif not args.no_fused_zero:
             bucket.fuse_zero_into(opt)  # the AdamW pass zeroes the bucket (no per-step fill)
+        if not self.sharded and world == 1:
+            # reference numerics: tcnn's f16 gradient rounding inside the AdamW pass (no-op
+            # in build numerics; with more ranks the all-reduce reads the rounded values)
+            pipe.defer_grad_quantize(opt)
         if not args.no_overlap and not self.sharded and not (graph and world > 1):
             # each chunk's all-reduce starts once its gradients are final: the surface and
             # MLP gradients reduce while the hash-grid backward runs

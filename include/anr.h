@@ -538,6 +538,10 @@ typedef struct anr_adam_tensor {
   float lr;
   float weight_decay;
   int64_t step;
+  /* > 0: the gradient is first rounded as tinycudann's f16 parameter gradient at this
+   * loss scale, g <- f16(f16(g * s) / s) (anr_grad_quantize_f16, fused into the update's
+   * read of g; reference numerics with a deferred quantisation). 0: g as it is. */
+  float grad_quant;
 } anr_adam_tensor;
 int anr_adam_step_multi(const anr_adam_tensor* tensors, int32_t n_tensors, float beta1,
                         float beta2, float eps, int32_t decoupled, int32_t zero_grad,

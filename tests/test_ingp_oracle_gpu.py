@@ -370,3 +370,55 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
         bar = 0.2 if n_samples == 1024 and row["iteration"] > 48 else 0.1
         assert abs(row["delta_reference_numerics_db"]) <= bar, rows
     assert rows[-1]["psnr_oracle"] > rows[0]["psnr_oracle"] + 1.0, rows
+
+
+def test_deferred_grad_quantize_same_update(scene, dev):
+    """defer_grad_quantize (bench.py's reference-numerics path): the end-of-backward pass
+    leaves the f32 sums in param.grad, and FusedAdam rounds them as tinycudann's f16
+    gradients while it reads them. From the same gradients (a copy of one backward's) the
+    deferred update equals quantise-then-update bit for bit, in the plain and the
+    capturable (device-step) forms. (Two separate backward passes are not compared: their
+    f32 atomics sum in different orders.)"""
+    from atmonr_amd import _lib
+    from atmonr_amd.batch_loader import BatchLoader
+    from atmonr_amd.optim import FusedAdam
+    from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
+
+    import __graft_entry__ as ge
+
+    p = InstantNGPPipeline(ge._ingp_config(N), scene, dtype=torch.float16, fused=True,
+                           seed=5, numerics="reference")
+    p.send_tensors_to(dev)
+    o = p.get_optimizer(OPT)
+    p.defer_grad_quantize(o)
+    b = next(iter(BatchLoader(scene, 128, seed=4)))
+    u = torch.rand(b["origin"].shape[0], N, generator=torch.Generator().manual_seed(6))
+    p.compute_loss(b, p.forward(b, u=u.to(dev))).backward()
+    torch.cuda.synchronize()
+    raw = {m: getattr(p, m).params.grad.clone() for m in ref_ingp.MODULES}
+    q = {}
+    for m, g in raw.items():
+        q[m] = g.clone()
+        _lib.call("anr_grad_quantize_f16", q[m].data_ptr(), q[m].numel(), 128.0, _lib.stream(dev))
+    torch.cuda.synchronize()
+    # the deferred pipeline left the sums unrounded
+    assert any(not torch.equal(raw[m], q[m]) for m in raw)
+    for capturable in (False, True):
+        out = []
+        for defer in (False, True):
+            ps = [torch.nn.Parameter(getattr(p, m).params.detach().clone()) for m in raw]
+            for t, m in zip(ps, raw):
+                t.grad = (raw[m] if defer else q[m]).clone()
+                if defer:
+                    t._anr_grad_quant = 128.0
+            opt = FusedAdam([{"params": ps[:1] + ps[3:4], "weight_decay": 0.0},
+                             {"params": ps[1:3] + ps[4:], "weight_decay": 1e-2}],
+                            lr=1e-2, betas=(0.9, 0.99), eps=1e-15, capturable=capturable)
+            for _ in range(2):
+                opt.step()
+            torch.cuda.synchronize()
+            out.append(ps)
+        for a_, b_ in zip(*out):
+            assert torch.equal(a_, b_)
+    with pytest.raises(ValueError):
+        p.defer_grad_quantize(torch.optim.AdamW(p.parameters(), lr=1e-3))

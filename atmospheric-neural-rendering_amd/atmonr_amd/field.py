@@ -200,6 +200,7 @@ class IngpFieldFn(torch.autograd.Function):
             # hash-grid backward (anr_hashgrid_bwd_count_requests on the same inputs)
             pipe._last_d_enc = d_enc
             pipe._last_hash_bwd = (coords, d_enc, g_hash)
+            pipe._last_field_grads = (d_sigma, d_color)
         call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
              _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
         _done(direct_h, p_hash)

@@ -799,12 +799,37 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
       }
     }
   };
+  // A batch whose dL/dy is zero in every lane (all 16 levels x 2 features of its BS
+  // samples: the reference numerics' f16 underflow leaves half of the 8-sample batches so
+  // at the bench state) adds nothing: its corners' pending sums are flushed as at a chunk
+  // end, the walk forgets its cell, and the batch is skipped. The same contributions reach
+  // the same entries (a pending sum may now arrive in two atomics instead of one: f32
+  // order, as any run). With skip_zero off (A/B) every batch is walked.
+  auto flush_all = [&]() {
+    if (have) {
+      uint32_t idx[NC];
+      LaneCorners<D>::indices(li, cell, b, idx);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        flush(acc[c] != 0.0f, idx[c], acc[c]);
+        acc[c] = 0.0f;
+      }
+      have = false;
+    }
+  };
   load_batch(m0, xb, gb);
   for (int64_t mb = m0; mb < m1; mb += BS) {
     load_batch(mb + BS, xn, gn);
+    bool nzb = false;
 #pragma unroll
-    for (int j = 0; j < BS; ++j)
-      if (mb + j < m1) step(xb[j], to_f32<TG>(gb[j]));
+    for (int j = 0; j < BS; ++j) nzb = nzb || (mb + j < m1 && to_f32<TG>(gb[j]) != 0.0f);
+    if (!skip_zero || __any(nzb)) {
+#pragma unroll
+      for (int j = 0; j < BS; ++j)
+        if (mb + j < m1) step(xb[j], to_f32<TG>(gb[j]));
+    } else {
+      flush_all();
+    }
 #pragma unroll
     for (int j = 0; j < BS; ++j) {
       gb[j] = gn[j];
@@ -812,12 +837,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
       for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
     }
   }
-  if (have) {
-    uint32_t idx[NC];
-    LaneCorners<D>::indices(li, cell, b, idx);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) flush(acc[c] != 0.0f, idx[c], acc[c]);
-  }
+  flush_all();
   if constexpr (COUNT) {
     // per lane (lanes above n_levels have returned; an instrument, not the hot path)
     if (n_req) atomicAdd(count, static_cast<unsigned long long>(n_req));

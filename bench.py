@@ -153,12 +153,26 @@ def count_hash_requests(job, n_samples: int) -> tuple[int, float] | None:
               g_hash.data_ptr(), cnt.data_ptr(), _lib.stream(coords.device))
     torch.cuda.synchronize()
     if os.environ.get("ANR_BENCH_DEBUG"):
+        ds_, dc_ = pipe._last_field_grads
+        M_ = ds_.shape[0]
+        up = (ds_.view(M_, -1) != 0).any(1) | (dc_.view(M_, -1) != 0).any(1)
+        for T_ in (8, 32, 256, 1024):
+            n_ = M_ // T_
+            print(f"[count_hash_requests] upstream-nonzero {T_}-row tiles "
+                  f"{up[:n_ * T_].view(n_, T_).any(1).float().mean().item():.4f} rows "
+                  f"{up.float().mean().item():.4f}", file=sys.stderr, flush=True)
+        dz_ = (d_enc != 0).any(1)
+        for T_ in (8, 32, 256):
+            n_ = M_ // T_
+            print(f"[count_hash_requests] d_enc-nonzero {T_}-row tiles "
+                  f"{dz_[:n_ * T_].view(n_, T_).any(1).float().mean().item():.4f}",
+                  file=sys.stderr, flush=True)
         print(f"[count_hash_requests] M={coords.shape[0]} coords {tuple(coords.shape)} "
               f"{coords.stride()} d_enc {tuple(d_enc.shape)} {d_enc.stride()} nonzero "
               f"{(d_enc != 0).float().mean().item():.4f} g_hash {g_hash.numel()} "
               f"count {int(cnt.item())}", file=sys.stderr, flush=True)
     nz = (d_enc != 0).float().mean().item()
-    del pipe._last_hash_bwd, pipe._last_d_enc
+    del pipe._last_hash_bwd, pipe._last_d_enc, pipe._last_field_grads
     return int(cnt.item()), nz
 
 

@@ -9,6 +9,16 @@ batch gather -> fused sampler/preprocessor -> hash grid -> MLPs -> composite -> 
 backward -> [RCCL all-reduce of the flat gradient when N > 1] -> fused AdamW.
 Data parallel over rays, one process per GPU, weak scaling (8192 rays per rank).
 
+Numerics: the headline runs the reference's own f16 arithmetic (``--numerics reference``:
+f16 composite and loss, tinycudann's x128 loss-scaled backward; the PSNR-parity path),
+started from 10 build-numerics steps (``warm_start``: the reference's f16 gradients never
+revive the density field that the first AdamW step kills on this scene, so a cold start
+would time a dead field); the build numerics are timed in the same run (``alt_numerics``).
+``d_enc_nonzero_frac`` reports how much of the step's dL/denc is nonzero (alive field).
+
+``--workload extract`` measures scripts/extract.py's loop (32,768 columns x 81 altitudes
+per batch, forward only) in points/s.
+
 ``--workload nerf`` measures BASELINE configs[1] instead (configs/nerf.json, batch 4096,
 f32 library GEMMs; see run_nerf). Rank 0 prints ONE JSON line. ``roofline`` is for the kernel that takes the most time per
 step, timed with HIP events on the launch stream inside the timed region; its

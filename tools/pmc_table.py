@@ -15,7 +15,7 @@ import sys
 
 KERNELS = {"hash_fwd": "hashgrid_fwd_v6_kernel<3, __half, __half>",
            "hash_fwd_v1": "hashgrid_fwd_kernel<3, 2, __half, __half>",
-           "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32>",
+           "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32, false>",
            "field_fwd": "field::fwd_kernel<64, 2, false, false, true>",
            "field_bwd": "field::bwd_rt_kernel<64, 2, true, false, false>",
            "sampler": "sample_uniform_bins_kernel",

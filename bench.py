@@ -836,6 +836,16 @@ def main():
         dom_stats = timer.summary().get(dominant)
     elif dominant and job.graphed:
         dom_stats = job.time_dominant(dominant, args.steps)
+    if req is not None and "hash_bwd" in models and world == 1:
+        # the field keeps learning through the timed steps (reference numerics: the
+        # nonzero share of dL/denc, and with it the requests, drift): count once more
+        # after them and price the roofline at the mean of the two counts
+        req2 = count_hash_requests(job, args.samples)
+        if req2 is not None:
+            hb = models["hash_bwd"]
+            hb["atomic_requests"] = 0.5 * (req[0] + req2[0])
+            hb["atomic_requests_before_after"] = [req[0], req2[0]]
+            hb["d_enc_nonzero_before_after"] = [round(req[1], 4), round(req2[1], 4)]
 
     strong = None
     if world > 1 and scaling == "weak" and not args.no_strong and args.batch % world == 0:
@@ -933,6 +943,9 @@ def main():
                 roofline["atomic_requests_per_launch"] = mdl["atomic_requests"]
                 roofline["atomic_requests_per_sample"] = round(mdl["atomic_requests"] / M, 4)
                 roofline["atomic_requests_source"] = mdl["atomic_requests_source"]
+                for x in ("atomic_requests_before_after", "d_enc_nonzero_before_after"):
+                    if x in mdl:
+                        roofline[x] = mdl[x]
                 if "atomic_requests_pmc" in mdl:
                     roofline["atomic_requests_pmc"] = mdl["atomic_requests_pmc"]
             if "atomic_requests_stale" in mdl:

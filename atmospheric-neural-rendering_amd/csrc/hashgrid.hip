@@ -781,14 +781,19 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
   const int col = level * 2 + f;
   auto load_batch = [&](int64_t mb, float (*xo)[D], TG* go) {
     if ((XS > 0 && DS > 0) && mb + BS <= m1) {  // wave-uniform: a full batch, no clamp
-      const float* __restrict__ xp = x + mb * XS;
+      // the batch's coordinates are the same for every lane: scalar loads through the
+      // constant address space (24 dwords: one s_load_dwordx16 + one x8) instead of 24
+      // vector loads of one broadcast dword each (hash bwd live 1.18 -> 1.06 ms, bench
+      // profiles/r04_hash_bwd_scalar_x_ab.log)
+      typedef __attribute__((address_space(4))) const float cf32;
+      const cf32* __restrict__ xp = (const cf32*)(x + mb * XS);
       const TG* __restrict__ dp = dout + mb * DS;
 #pragma unroll
-      for (int j = 0; j < BS; ++j) {
+      for (int j = 0; j < BS; ++j)
 #pragma unroll
         for (int d = 0; d < D; ++d) xo[j][d] = xp[j * XS + d];
-        go[j] = dp[j * DS + col];
-      }
+#pragma unroll
+      for (int j = 0; j < BS; ++j) go[j] = dp[j * DS + col];
     } else {
 #pragma unroll
       for (int j = 0; j < BS; ++j) {

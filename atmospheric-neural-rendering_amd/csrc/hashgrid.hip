@@ -706,6 +706,14 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
   float* __restrict__ grad = dtable + static_cast<int64_t>(G.offset[level]) * 2 + f;
   LevelIdx<D> li;
   li.init(T, res);
+  // The flushes are buffer atomics whose non-flushing lanes get an offset past the
+  // table: the hardware range check drops them, so a flush is one select and one atomic
+  // instruction, not a divergent branch (exec save / test / restore: scalar instructions,
+  // which bounded this walk — SQ counters, profiles/r04_sq_close.md)
+  const uint32_t table_bytes = (G.offset[n_levels - 1] + G.size[n_levels - 1]) * 8u;
+  const __amdgpu_buffer_rsrc_t rg = wave_rsrc(dtable, table_bytes);
+  const uint32_t gbase = (G.offset[level] * 2u + static_cast<uint32_t>(f)) * 4u;
+  constexpr uint32_t kDrop = 0x80000000u;  // >= table_bytes (ABI: tables < 2 GB)
 
   uint32_t cell[D];
   bool have = false;
@@ -719,8 +727,8 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     if constexpr (COUNT) {
       n_req += distinct_segments(
           out, reinterpret_cast<uintptr_t>(grad + static_cast<int64_t>(e) * 2) >> 6);
-    } else {
-      if (out && (HASH_EXP & 1) == 0) atomicAdd(grad + static_cast<int64_t>(e) * 2, v);
+    } else if constexpr ((HASH_EXP & 1) == 0) {
+      __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rg, out ? gbase + e * 8u : kDrop, 0, 0);
     }
   };
 

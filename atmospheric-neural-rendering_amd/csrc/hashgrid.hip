@@ -1012,7 +1012,11 @@ template <int D, int F>
 static int launch_bwd(const GridLevels& G, const anr_hashgrid_desc* d, const float* x,
                       int64_t x_stride, int64_t M, const void* dout, int32_t gdt,
                       int64_t dout_stride, float* dtable, hipStream_t s) {
-  if (F == 2 && d->n_levels <= 16 && bwd_v2()) {
+  // v2 addresses the gradient table through a buffer descriptor (32-bit byte offsets, the
+  // drop offset at 2 GB): larger tables (2^24 entries x 16 levels) take the v1 walker
+  const uint64_t grad_bytes =
+      (static_cast<uint64_t>(G.offset[d->n_levels - 1]) + G.size[d->n_levels - 1]) * F * 4u;
+  if (F == 2 && d->n_levels <= 16 && grad_bytes < 0x80000000ull && bwd_v2()) {
     const int64_t K = pick_chunk_v2(M);
     const int64_t waves = ceil_div(M, K);
     const dim3 grid(static_cast<unsigned>(ceil_div(waves, 4))), block(256);

@@ -332,9 +332,13 @@ class KernelTimer:
         torch.cuda.synchronize()
         out = {}
         for name, evs in self.events.items():
-            ts = [a.elapsed_time(b) for a, b in evs]
+            ts = [e[0].elapsed_time(e[1]) for e in evs]
             out[name] = {"launches": len(ts), "total_ms": sum(ts),
-                         "avg_ms": sum(ts) / max(1, len(ts))}
+                         "avg_ms": sum(ts) / max(1, len(ts)),
+                         # launches on a side stream (the surface branch, _surface_async):
+                         # their event time runs beside the main chain and includes
+                         # waiting for CU slots there, so it is not a step cost
+                         "side_stream_launches": sum(1 for e in evs if e[2])}
         return out
 
 
@@ -372,7 +376,9 @@ def call(name: str, *args, tag: str | None = None) -> int:
         a.record()
         rc = getattr(lib, name)(*args)
         b.record()
-        _timer.events.setdefault(tag or name, []).append((a, b))
+        cur = torch.cuda.current_stream()
+        side = any(cur == st for st in _side_streams.values())
+        _timer.events.setdefault(tag or name, []).append((a, b, side))
     else:
         rc = getattr(lib, name)(*args)
     if rc != 0:

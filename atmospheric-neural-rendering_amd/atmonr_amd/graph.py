@@ -95,19 +95,38 @@ class GraphedTrainStep:
         finally:
             _lib._timer = saved
         self.graph = g
+        self._opt_generation = getattr(self.optimizer, "generation", 0)
         if self.bucket is not None and self.optimizer_in_graph:
             # the captured AdamW zeroes the bucket in its pass (or the graph's own fill
             # does): eager code after a replay sees zero gradients
             self.bucket._known_zero = True
 
+    def _refresh_compute_copies(self) -> None:
+        """A parameter torch modified since the capture (a checkpoint's load_state_dict,
+        ``copy_``) has a stale f16 compute copy: the replay reads the copy, and only the
+        eager forward would notice the version change. Rewrite such copies in place (same
+        storage, so the graph's pointers stay valid) before replaying."""
+        for group in self.optimizer.param_groups:
+            for p in group["params"]:
+                sh = getattr(p, "_anr_shadow", None)
+                if sh is not None and getattr(p, "_anr_shadow_ver", None) != p._version:
+                    _lib.compute_copy(p, sh.dtype)
+
     def __call__(self, idx: torch.Tensor) -> torch.Tensor:
         """One step on rows ``idx`` (device int64, the captured batch size)."""
+        if (self.graph is not None and self.optimizer_in_graph
+                and getattr(self.optimizer, "generation", 0) != self._opt_generation):
+            # the optimizer replaced tensors the graph points at (e.g. a load_state_dict
+            # that could not copy in place): rebuild its device state eagerly, recapture
+            self.graph = None
+            self.optimizer._prepare()
         if self.graph is None:
             self.capture(idx)
         elif idx.data_ptr() != self.static_idx.data_ptr():
             self.static_idx.copy_(idx)
         if self.optimizer_in_graph:
             self.optimizer.sync_hyper()
+        self._refresh_compute_copies()
         self.graph.replay()
         if self.after is not None:
             self.after()

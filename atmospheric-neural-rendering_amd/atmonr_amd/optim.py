@@ -46,6 +46,9 @@ class FusedAdam(torch.optim.Optimizer):
         self.multi_tensor = True  # one anr_adam_step_multi launch per step and device
         self.capturable = capturable
         self._devstate: dict = {}  # capturable: (device, b1, b2, eps) -> device step / lr
+        # bumped whenever tensors a captured step points at (the device step / lr / scratch,
+        # or exp_avg / exp_avg_sq storage) are replaced: GraphedTrainStep recaptures then
+        self.generation = 0
 
     # ------------------------------------------------------------------ capturable mode
     def _entries(self):
@@ -81,40 +84,58 @@ class FusedAdam(torch.optim.Optimizer):
                 ds["lr"].copy_(torch.tensor(lrs, dtype=torch.float32))
                 ds["lr_host"] = lrs
 
+    def _signature(self):
+        return tuple((k, id(p), id(g)) for k, p, g in self._entries())
+
     def _prepare(self):
         """Device step / lr buffers per launch key, built eagerly (never inside a capture:
-        their initial values must not be part of the graph)."""
-        batches: dict = {}
-        for key, p, group in self._entries():
-            batches.setdefault(key, []).append((p, group))
-        if set(batches) != set(self._devstate):
+        their initial values must not be part of the graph). The kernel reads tensor t's lr
+        from d_lr[t] in launch order, so the state is rebuilt whenever the ordered list of
+        (parameter, group) with gradients changes -- not only when the key set does (a
+        parameter gaining / losing its grad, or moving between groups of equal betas).
+        A rebuild first writes the device step counts back to the host state, and groups
+        parameters by step count (a parameter that skipped steps keeps its own count, as
+        torch's per-parameter ``step``)."""
+        sig = self._signature()
+        if sig != getattr(self, "_sig", None) or not self._devstate:
             if torch.cuda.is_current_stream_capturing():
-                raise _lib.ANRError("FusedAdam(capturable=True): run one step eagerly before "
-                                    "capturing it (the device step/lr state is built then)")
+                raise _lib.ANRError("FusedAdam(capturable=True): the parameters with gradients "
+                                    "changed since the device step/lr state was built; run one "
+                                    "step eagerly before capturing")
+            self._sync_host_steps()
             self._devstate = {}
-            for key, items in batches.items():
-                if len(items) > _lib.ADAM_DEV_MAX_TENSORS:
+            self.generation += 1
+            for key_hp, p, group in self._entries():
+                st = self._init_state(p)
+                key = key_hp + (int(st["step"].item()),)
+                self._devstate.setdefault(key, {"params": [], "groups": []})
+                self._devstate[key]["params"].append(p)
+                self._devstate[key]["groups"].append(group)
+            for key, ds in self._devstate.items():
+                if len(ds["params"]) > _lib.ADAM_DEV_MAX_TENSORS:
                     raise _lib.ANRError(f"capturable FusedAdam: at most "
                                         f"{_lib.ADAM_DEV_MAX_TENSORS} tensors per launch")
                 dev = key[0]
-                sts = [self._init_state(p) for p, _ in items]
-                step0 = int(sts[0]["step"].item())
-                if any(int(st["step"].item()) != step0 for st in sts):
-                    raise _lib.ANRError("capturable FusedAdam: parameters at different steps")
-                self._devstate[key] = {
-                    "params": [p for p, _ in items], "groups": [g for _, g in items],
-                    "step": torch.tensor([step0], dtype=torch.int64, device=dev),
-                    "lr": torch.tensor([float(g["lr"]) for _, g in items], device=dev),
-                    "lr_host": [float(g["lr"]) for _, g in items],
-                    "scratch": torch.zeros(3 * _lib.ADAM_DEV_MAX_TENSORS, device=dev)}
-        return batches
+                lrs = [float(g["lr"]) for g in ds["groups"]]
+                ds.update({"step": torch.tensor([key[4]], dtype=torch.int64, device=dev),
+                           "lr": torch.tensor(lrs, device=dev), "lr_host": lrs,
+                           "scratch": torch.zeros(3 * _lib.ADAM_DEV_MAX_TENSORS, device=dev)})
+            self._sig = sig
+        return {k: list(zip(ds["params"], ds["groups"])) for k, ds in self._devstate.items()}
+
+    def _sync_host_steps(self) -> None:
+        """Device step counts -> state[p]["step"] (host); synchronises."""
+        for ds in self._devstate.values():
+            n = float(ds["step"].item())
+            for p in ds["params"]:
+                self.state[p]["step"] = torch.tensor(n)
 
     def _step_capturable(self):
         batches = self._prepare()
         if not torch.cuda.is_current_stream_capturing():
             self.sync_hyper()
         for key, items in batches.items():
-            dev, b1, b2, eps = key
+            dev, b1, b2, eps = key[:4]
             ds = self._devstate[key]
             ts = []
             for p, group in items:
@@ -139,15 +160,60 @@ class FusedAdam(torch.optim.Optimizer):
 
     def state_dict(self):
         if self.capturable:
-            for ds in self._devstate.values():
-                n = float(ds["step"].item())
-                for p in ds["params"]:
-                    self.state[p]["step"] = torch.tensor(n)
+            self._sync_host_steps()
         return super().state_dict()
 
     def load_state_dict(self, state_dict):
+        """torch's load replaces the state tensors and the param-group dicts. In capturable
+        mode with device state built, the loaded values are copied INTO the existing
+        exp_avg / exp_avg_sq / device step / lr storage instead, so a captured step
+        (GraphedTrainStep) keeps pointing at live memory and replays from the loaded state.
+        When that is impossible (new parameters, shapes, mixed steps) the device state is
+        dropped and ``generation`` bumped: a graph built on it recaptures before replaying."""
+        if not (self.capturable and self._devstate):
+            super().load_state_dict(state_dict)
+            self._devstate = {}  # rebuilt from the loaded host steps at the next step()
+            self.generation += 1
+            return
+        old = {p: (st.get("exp_avg"), st.get("exp_avg_sq")) for p, st in self.state.items()}
         super().load_state_dict(state_dict)
-        self._devstate = {}  # rebuilt from the loaded host steps at the next step()
+        ok = True
+        with torch.no_grad():
+            for p, st in self.state.items():
+                o = old.get(p)
+                new_ = (st.get("exp_avg"), st.get("exp_avg_sq"))
+                if (o is None or any(t is None for t in o + new_)
+                        or any(a.shape != b.shape or a.dtype != b.dtype or a.device != b.device
+                               for a, b in zip(o, new_))):
+                    ok = False
+                    break
+                o[0].copy_(new_[0])
+                o[1].copy_(new_[1])
+                st["exp_avg"], st["exp_avg_sq"] = o
+                if st["step"].device.type != "cpu":
+                    st["step"] = st["step"].cpu()
+            group_of = {id(p): g for g in self.param_groups for p in g["params"]}
+            for ds in (self._devstate.values() if ok else ()):
+                if any(id(p) not in group_of or p not in self.state for p in ds["params"]):
+                    ok = False
+                    break
+                steps = {int(self.state[p]["step"].item()) for p in ds["params"]}
+                if len(steps) != 1:
+                    ok = False
+                    break
+                ds["step"].fill_(steps.pop())
+                ds["groups"] = [group_of[id(p)] for p in ds["params"]]
+                ds["lr_host"] = None  # sync_hyper rewrites the lr tensor in place
+        if ok:
+            # same parameters in the same launch order; only the group dicts are new
+            old_sig = [(k, i) for k, i, _ in self._sig]
+            ok = [(k, id(p)) for k, p, _ in self._entries()] == old_sig
+        if ok:
+            self._sig = self._signature()
+            self.sync_hyper()
+        else:
+            self._devstate = {}
+            self.generation += 1
 
     @torch.no_grad()
     def step(self, closure=None):

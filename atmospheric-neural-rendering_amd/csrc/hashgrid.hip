@@ -757,9 +757,9 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
         LaneCorners<D>::carry(acc, dl, keepx, nacc);
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          // no test of acc != 0 here: a leaving corner's sum is zero only when its
-          // weights were (samples exactly on the cell faces), and the per-corner test
-          // cost more instructions than the rare zero requests it saves
+          // skip_zero: a leaving corner whose sum is exactly zero issues no request
+          // (reference numerics: tcnn's x128 f16 backward rounds most dL/denc to zero);
+          // without skip_zero only the leaving test applies
           const bool out = (!keepx || LaneCorners<D>::leaves(c, dl)) &&
                            (!skip_zero || acc[c] != 0.0f);
           flush(out, idx[c], acc[c]);
@@ -814,10 +814,12 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
   };
   // A batch whose dL/dy is zero in every lane (all 16 levels x 2 features of its BS
   // samples: the reference numerics' f16 underflow leaves half of the 8-sample batches so
-  // at the bench state) adds nothing: its corners' pending sums are flushed as at a chunk
-  // end, the walk forgets its cell, and the batch is skipped. The same contributions reach
-  // the same entries (a pending sum may now arrive in two atomics instead of one: f32
-  // order, as any run). With skip_zero off (A/B) every batch is walked.
+  // at the bench state) adds nothing and is skipped with one test. skip_zero 2 (default)
+  // also skips single all-zero samples inside a batch and keeps the pending cell across
+  // the skipped ones; skip_zero 1 (the r04 form, A/B) walks every sample of a batch with
+  // any nonzero value and flushes at an all-zero batch as at a chunk end. Either way the
+  // same contributions reach the same entries (a pending sum may arrive in two atomics
+  // instead of one: f32 order, as any run). With skip_zero 0 (A/B) every batch is walked.
   auto flush_all = [&]() {
     if (have) {
       uint32_t idx[NC];
@@ -838,9 +840,15 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     for (int j = 0; j < BS; ++j) nzb = nzb || (mb + j < m1 && to_f32<TG>(gb[j]) != 0.0f);
     if (!skip_zero || __any(nzb)) {
 #pragma unroll
-      for (int j = 0; j < BS; ++j)
-        if (mb + j < m1) step(xb[j], to_f32<TG>(gb[j]));
-    } else {
+      for (int j = 0; j < BS; ++j) {
+        const float gv = to_f32<TG>(gb[j]);
+        // skip_zero 2: a SAMPLE whose dL/dy row is zero in every lane (all levels and
+        // features) is not walked at all: it adds nothing, and the walk stays exact
+        // because the next walked sample's cell test / carry handles any jump (every
+        // corner leaves when a coordinate moves by more than one cell)
+        if (mb + j < m1 && (skip_zero < 2 || __any(gv != 0.0f))) step(xb[j], gv);
+      }
+    } else if (skip_zero == 1) {
       flush_all();
     }
 #pragma unroll
@@ -999,11 +1007,13 @@ static int launch_fwd(const GridLevels& G, const anr_hashgrid_desc* d, const flo
 // reference numerics most samples' f16 dL/denc underflow to zero (tcnn's x128 loss scale
 // rounds them away), and the memory-side request count at the chunk ends alone fell from
 // 20.8 M to 18.7 M per launch after the first step (profiles/r04_close PMC).
-// ANR_HASH_SKIP0 = 0 / 1 overrides (A/B hook); default on.
+// ANR_HASH_SKIP0 = 0 / 1 / 2 overrides (A/B hook); default 2 (per-sample skip of
+// all-zero dL/dy rows, r05).
 static int bwd_skip_zero() {
   static const int v = [] {
     const char* e = getenv("ANR_HASH_SKIP0");
-    return e ? (atoi(e) != 0) : 1;
+    const int k = e ? atoi(e) : 2;
+    return k < 0 ? 0 : (k > 2 ? 2 : k);
   }();
   return v;
 }
@@ -1147,9 +1157,18 @@ extern "C" int anr_hashgrid_bwd_count_requests(const anr_hashgrid_desc* d, const
               "levels) is instrumented");
     return ANR_E_UNSUPPORTED;
   }
-  if (M == 0) return ANR_OK;
   GridLevels G;
   ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_bwd_count_requests: descriptor not initialised");
+  // the same gate as launch_bwd: gradient tables of 2 GB or more take the v1 walker there,
+  // whose requests this v2 instrument does not model
+  const uint64_t grad_bytes =
+      (static_cast<uint64_t>(G.offset[d->n_levels - 1]) + G.size[d->n_levels - 1]) * 2u * 4u;
+  if (grad_bytes >= 0x80000000ull) {
+    set_error("anr_hashgrid_bwd_count_requests: gradient table of 2 GB or more (the backward "
+              "runs the uninstrumented v1 walker there)");
+    return ANR_E_UNSUPPORTED;
+  }
+  if (M == 0) return ANR_OK;
   const int64_t K = pick_chunk_v2(M);
   const dim3 grid(static_cast<unsigned>(ceil_div(ceil_div(M, K), 4))), block(256);
   float* tab = const_cast<float*>(dtable);  // not written in COUNT mode

@@ -2,9 +2,10 @@
 
 bench.py's ``cpu_baseline`` leg: the reference's own CPU-runnable configuration
 (BASELINE.json configs[0]: nerf.json's pipeline on an 8-view 64x64 synthetic scene), run
-with oracle/ref_nerf.py on the host cores at batch 1,024 (nerf.json trains at 4,096;
-rays/s of the NeRF step is flat in the batch on the CPU, SURVEY §6: 280-360 at 256 and
-~350 at 4,096) so the bounded sample fits bench.py's time budget. Returns rays/s.
+with oracle/ref_nerf.py on the host cores at nerf.json's own batch of 4,096 rays
+(r05 -- r01-r04 used 1,024), one warm-up step and up to three timed ones,
+so the bounded sample stays within bench.py's time budget. Returns rays/s and where the
+thread count came from.
 """
 
 from __future__ import annotations
@@ -15,18 +16,36 @@ import time
 import torch
 
 
-def run(budget_s: float = 40.0, batch_size: int = 1024, threads: int | None = None,
-        seed: int = 0, warmup: int = 2, timed: int = 5) -> dict:
+def host_threads(threads: int | None = None) -> tuple[int, str]:
+    """The host share the job may use, and where that number came from: OMP_NUM_THREADS
+    (the GPU box sets it to its per-GPU share of 16; os.cpu_count() there counts the whole
+    machine), else the process's CPU affinity mask."""
+    if threads is not None:
+        return threads, "argument"
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env), "OMP_NUM_THREADS"
+    try:
+        return len(os.sched_getaffinity(0)), "len(os.sched_getaffinity(0))"
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1, "os.cpu_count()"
+
+
+def _affinity() -> int | None:
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+
+
+def run(budget_s: float = 45.0, batch_size: int = 4096, threads: int | None = None,
+        seed: int = 0, warmup: int = 1, timed: int = 3) -> dict:
     """Median rays/s of ``timed`` train steps after ``warmup`` (stops early at
-    ``budget_s``). Threads: the host share the job may use (OMP_NUM_THREADS, which the GPU
-    box sets to its per-GPU share of 16; os.cpu_count() there counts the whole machine),
-    else min(16, os.cpu_count())."""
+    ``budget_s``) on ``host_threads()`` threads."""
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
     from oracle.ref_nerf import RefNeRFPipeline
 
-    if threads is None:
-        env = os.environ.get("OMP_NUM_THREADS", "")
-        threads = int(env) if env.isdigit() and int(env) > 0 else min(16, os.cpu_count() or 1)
+    threads, source = host_threads(threads)
     torch.set_num_threads(threads)
     torch.manual_seed(seed)
     ds = SyntheticHARP2Dataset(n_views=8, img_size=64, device="cpu", seed=seed)
@@ -61,6 +80,8 @@ def run(budget_s: float = 40.0, batch_size: int = 1024, threads: int | None = No
         "value": batch_size / med,
         "unit": "rays/s",
         "cores": threads,
+        "cores_source": source,
+        "affinity_cpus": _affinity(),
         "host_cpus": os.cpu_count(),
         "kind": "port",
         "sample": (f"configs/nerf.json train step (coarse 64 + fine 128 samples, 8x256 MLP, "
@@ -82,9 +103,7 @@ def run_extract(budget_s: float = 20.0, n_points: int = 131072, threads: int | N
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
     from oracle import ref_nerf, ref_tcnn
 
-    if threads is None:
-        env = os.environ.get("OMP_NUM_THREADS", "")
-        threads = int(env) if env.isdigit() and int(env) > 0 else min(16, os.cpu_count() or 1)
+    threads, source = host_threads(threads)
     torch.set_num_threads(threads)
     gen = torch.Generator().manual_seed(seed)
     ds = SyntheticHARP2Dataset(n_views=8, img_size=64, device="cpu", seed=seed)
@@ -123,6 +142,7 @@ def run_extract(budget_s: float = 20.0, n_points: int = 131072, threads: int | N
     med = times[len(times) // 2]
     return {
         "value": n_points / med, "unit": "points/s", "cores": threads,
+        "cores_source": source, "affinity_cpus": _affinity(),
         "host_cpus": os.cpu_count(), "kind": "port",
         "sample": (f"extract loop body (f64 preprocessor, tcnn hash grid T=2^19 and 2x64 "
                    f"pos MLP restated in numpy / torch CPU) on {n_points} random in-scene "

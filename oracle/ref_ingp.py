@@ -46,6 +46,18 @@ its f16 Instant-NGP path, as opposed to what this build computes:
 Approximations (tcnn absent): the MLP backward's rounding is applied per layer, not per
 16x16 tile; the hash-grid gradient (tcnn: f16 half2 atomics) is summed in f64 and
 rounded once.
+
+``acc`` (reference semantics): the accumulation precision of the sums that feed each f16
+rounding -- the MLP products (forward, dL/dx, dL/dW) and the hash grid's trilinear sums
+and gradient scatter. tcnn's kernels accumulate in f32 (MMA / atomics) in an order of
+their own, which no CPU restatement can reproduce; the arms are equally valid orders:
+``"f64"`` (default) sums exactly enough that each f16 rounding sees the exact value;
+``"f32"`` sums in f32 in torch-CPU's BLAS / index_add order (the GPU's precision, its
+own order); ``"f32rev"`` sums in f32 with every reduction axis reversed (a third order).
+Near f16's subnormal range a sum with cancellation rounds differently under f32 than
+under f64, and AdamW with eps = 1e-15 turns a gradient that is 0 in one order and one
+subnormal in another into a full lr step of a never-touched entry: the arms measure how
+far the reference's own PSNR trajectory depends on its summation order.
 """
 
 from __future__ import annotations
@@ -63,16 +75,82 @@ def _grid_cfg(enc_cfg: dict, n_dims: int):
             float(enc_cfg["per_level_scale"]), int(enc_cfg["log2_hashmap_size"]))
 
 
-def hashgrid(x: torch.Tensor, table: torch.Tensor, cfg, rnd) -> torch.Tensor:
-    """tcnn GridEncoding forward, differentiable in ``table``; x (M, D) float32."""
+def hashgrid(x: torch.Tensor, table: torch.Tensor, cfg, rnd, acc: str = "f64") -> torch.Tensor:
+    """tcnn GridEncoding forward, differentiable in ``table``; x (M, D) float32. ``acc``
+    "f32" / "f32rev": the corner sums and the gradient scatter in f32 (reversed sample
+    order for the scatter with "f32rev")."""
     xn = x.detach().float().numpy()
     tab = rnd(table).view(-1, 2)
+    if acc != "f64":
+        tab = _Cast.apply(tab, torch.float32)
     outs = []
     for lvl in range(cfg[1]):
         idx, wt = ref_tcnn.hashgrid_corners(xn, cfg, lvl)
-        outs.append(torch.einsum("mc,mcf->mf", torch.from_numpy(wt),
-                                 tab[torch.from_numpy(idx)]))
-    return rnd(torch.cat(outs, dim=1))
+        wt_t = torch.from_numpy(wt).to(tab.dtype)
+        idx_t = torch.from_numpy(idx)
+        if acc == "f32rev":
+            rev = torch.arange(idx_t.shape[0] - 1, -1, -1)
+            g = _FlipGather.apply(tab, idx_t, rev)
+        else:
+            g = tab[idx_t]
+        outs.append(torch.einsum("mc,mcf->mf", wt_t, g))
+    return rnd(torch.cat(outs, dim=1).double())
+
+
+class _Cast(torch.autograd.Function):
+    """x -> x.to(dtype); the gradient comes back in x's dtype (value of the f32 sum)."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.dt = x.dtype
+        return x.to(dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dt), None
+
+
+class _FlipGather(torch.autograd.Function):
+    """tab[idx] whose backward scatters the samples in reversed order (f32rev arm)."""
+
+    @staticmethod
+    def forward(ctx, tab, idx, rev):
+        ctx.save_for_backward(idx, rev)
+        ctx.n = tab.shape[0]
+        return tab[idx]
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, rev = ctx.saved_tensors
+        out = torch.zeros((ctx.n,) + tuple(g.shape[2:]), dtype=g.dtype)
+        out.index_add_(0, idx[rev].reshape(-1), g[rev].reshape(-1, *g.shape[2:]))
+        return out, None, None
+
+
+class _MatmulAcc(torch.autograd.Function):
+    """h @ W.t() with every sum of the forward and the backward in f32 (``rev``: each
+    reduction axis reversed) -- the f32 / f32rev arms of RefInstantNGP(acc=...)."""
+
+    @staticmethod
+    def forward(ctx, h, W, rev):
+        ctx.save_for_backward(h, W)
+        ctx.rev = rev
+        hf, Wf = h.float(), W.float()
+        if rev:
+            hf, Wf = hf.flip(1), Wf.flip(1)
+        return (hf @ Wf.t()).double()
+
+    @staticmethod
+    def backward(ctx, g):
+        h, W = ctx.saved_tensors
+        gf, hf, Wf = g.float(), h.float(), W.float()
+        if ctx.rev:
+            dh = gf.flip(1) @ Wf.flip(0)
+            dW = gf.flip(0).t() @ hf.flip(0)
+        else:
+            dh = gf @ Wf
+            dW = gf.t() @ hf
+        return dh.double(), dW.double(), None
 
 
 LOSS_SCALE = 128.0  # tinycudann.modules default loss scale for f16 parameters
@@ -162,7 +240,7 @@ class RefInstantNGP:
 
     def __init__(self, config: dict, state: dict, prep: dict, scale: float, max_i: float,
                  half: bool = False, mlp_half=None, semantics: str = "build",
-                 composite: str = "f32", ref_acc: str = "cuda"):
+                 composite: str = "f32", ref_acc: str = "cuda", acc: str = "f64"):
         self.cfg = config
         self.ingp = config["instant_ngp"]
         self.N = int(config["num_samples_per_ray"])
@@ -182,6 +260,9 @@ class RefInstantNGP:
         # reference semantics: torch's CUDA ("cuda", ref_f16) or CPU ("cpu", torch ops)
         # f16 composite / loss kernels
         self.ref_acc = ref_acc
+        if acc not in ("f64", "f32", "f32rev"):
+            raise ValueError(f"acc={acc!r}: f64, f32 or f32rev")
+        self.acc = acc  # reference semantics: accumulation arm (module docstring)
         self.params = {m: state[m]["params"].detach().cpu().double().clone().requires_grad_(True)
                        for m in MODULES}
         self.pos_grid = _grid_cfg(self.ingp["encoding"], 3)
@@ -245,7 +326,7 @@ class RefInstantNGP:
         for k, (o, i) in enumerate(shapes):
             W = p[off:off + o * i].half().double().view(o, i)
             off += o * i
-            h = h @ W.t()
+            h = h @ W.t() if self.acc == "f64" else _MatmulAcc.apply(h, W, self.acc == "f32rev")
             if k < len(shapes) - 1:
                 # f16 tile: relu, rounded value and gradient, mask on the stored f16
                 # activation (tcnn's ReLU backward)
@@ -257,7 +338,7 @@ class RefInstantNGP:
 
     def _grid_ref(self, cfg):
         def fn(x, p):
-            return hashgrid(x, p, cfg, lambda t: t.half().double())
+            return hashgrid(x, p, cfg, lambda t: t.half().double(), self.acc)
         return fn
 
     def _forward_reference(self, b: dict, u) -> dict:

@@ -117,3 +117,94 @@ def test_graphed_step_matches_eager(scene, dev):
     for n, a in params[False].items():
         b = params[True][n]
         assert torch.linalg.norm(a - b) <= PARAM_RTOL * torch.linalg.norm(a), n
+
+
+def test_graph_replay_after_load_state_dict(dev):
+    """a checkpoint loaded into a capturable FusedAdam while a captured update
+    is live. The loaded moments / step / lr are copied into the storage the graph points
+    at, so replays continue from the loaded state: the update replayed for steps 3-4 after
+    restoring the step-2 checkpoint (parameters + optimizer state) equals steps 3-4 of the
+    uninterrupted run bit for bit, and no recapture is needed (same generation). (The
+    whole train step is not compared this way: its stratified draws come from the device
+    RNG, which a restore does not rewind.)"""
+    import copy
+
+    from atmonr_amd.optim import FusedAdam
+
+    torch.manual_seed(3)
+    shapes = [(4096,), (300, 7), (64,)]
+    ps = [torch.nn.Parameter(torch.randn(s, device=dev)) for s in shapes]
+    grads = [[torch.randn(s, device=dev) for s in shapes] for _ in range(5)]
+    opt = FusedAdam([{"params": ps[:2], "weight_decay": 0.0},
+                     {"params": ps[2:], "weight_decay": 1e-2}], lr=1e-2, betas=(0.9, 0.99),
+                    eps=1e-15, capturable=True)
+    for q, gr in zip(ps, grads[0]):
+        q.grad = gr.clone()
+    opt.step()  # eager: builds the device step / lr state
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        opt.step()
+
+    def replay(k):
+        for q, gr in zip(ps, grads[k]):
+            q.grad.copy_(gr)
+        opt.sync_hyper()
+        graph.replay()
+
+    for k in (1, 2):
+        replay(k)
+    torch.cuda.synchronize()
+    ck_params = [q.detach().clone() for q in ps]
+    ck_opt = copy.deepcopy(opt.state_dict())
+    gen0 = opt.generation
+    for k in (3, 4):
+        replay(k)
+    ref = [q.detach().clone() for q in ps]
+    with torch.no_grad():
+        for q, c in zip(ps, ck_params):
+            q.copy_(c)
+    opt.load_state_dict(ck_opt)
+    assert opt.generation == gen0  # copied in place: the captured graph stays valid
+    for k in (3, 4):
+        replay(k)
+    torch.cuda.synchronize()
+    assert opt.device_step() == 5
+    for a, q in zip(ref, ps):
+        assert torch.equal(a, q.detach())
+    # a lr written by a scheduler after the load still reaches the captured update
+    for gp in opt.param_groups:
+        gp["lr"] *= 0.5
+    replay(4)
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(q).all() for q in ps)
+
+
+def test_adam_dev_rebuilds_when_grads_change(dev):
+    """the device lr table follows launch order, so a parameter that loses its
+    gradient (or gains one) must rebuild the capturable state, not shift every later
+    tensor onto another tensor's lr. Capturable and plain FusedAdam stay bit-identical
+    through such a change, and the rebuild bumps ``generation`` (a live graph would
+    recapture)."""
+    from atmonr_amd.optim import FusedAdam
+
+    torch.manual_seed(1)
+    shapes = [(100,), (300,), (50,)]
+    init = [torch.randn(s, device=dev) for s in shapes]
+    grads = [[torch.randn(s, device=dev) for s in shapes] for _ in range(4)]
+    out = []
+    gens = []
+    for capturable in (False, True):
+        ps = [torch.nn.Parameter(x.clone()) for x in init]
+        opt = FusedAdam([{"params": ps[:1], "lr": 1e-2}, {"params": ps[1:], "lr": 3e-3}],
+                        betas=(0.9, 0.99), eps=1e-15, weight_decay=0.0, capturable=capturable)
+        for k in range(4):
+            for j, (q, gr) in enumerate(zip(ps, grads[k])):
+                # step 2: the first parameter has no gradient (skipped by both forms)
+                q.grad = None if (k == 2 and j == 0) else gr.clone()
+            opt.step()
+            gens.append(opt.generation) if capturable else None
+        out.append([q.detach().clone() for q in ps])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+    assert gens[2] > gens[1] and gens[3] > gens[2]  # rebuilt at the change and back

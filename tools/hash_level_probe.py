@@ -5,7 +5,7 @@ for every level l, a ONE-level grid with exactly level l's table size, resolutio
 scale (its own table, offset 0), and every consecutive level pair (2p, 2p+1) likewise,
 run through the same anr_hashgrid_fwd entry point.
 
-Under rocprofv3 --pmc (tools/r3_hash_level_pmc.sh) the hashgrid_fwd dispatches come in
+Under rocprofv3 --pmc (tools/archive/r3_hash_level_pmc.sh) the hashgrid_fwd dispatches come in
 the order printed as "launch_order", so each PMC row maps to (level | full, rep). The
 one-level runs show what each level costs when it has the L2 to itself; the sum over
 levels against the full run is the cross-level interference.

@@ -1,5 +1,5 @@
 """Join tools/hash_level_probe.py's launch order with the rocprofv3 --pmc passes of
-tools/r3_hash_level_pmc.sh: per (grid, rep) duration, TCC hit/miss, FETCH_SIZE and
+tools/archive/r3_hash_level_pmc.sh: per (grid, rep) duration, TCC hit/miss, FETCH_SIZE and
 WRITE_SIZE per sample. FETCH_SIZE is printed raw and calibrated: 4-B gathers count one
 64-B unit per TCC miss (profiles/r03_gather_calib), the 12-B/sample coordinate stream is
 half-counted (MI355X_MICROARCH.md), so calibrated fetch = raw + 6 B/sample.

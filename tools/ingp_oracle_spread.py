@@ -50,7 +50,8 @@ def main():
                     "f32master: one run with f32 parameters / AdamW moments (the "
                     "reference's) beside the oracle's f64 masters; gradnoise: per-step "
                     "relative gradient noise of --noise; sumnoise: the hash grid gradient "
-                    "with --noise x u_f32 x sum|terms| of f32 summation-order noise")
+                    "with --noise x u_f32 x sum|terms| of f32 summation-order noise; "
+                    "acc: the f32 and f32rev accumulation arms of oracle/ref_ingp.py")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     import __graft_entry__ as ge
@@ -78,6 +79,15 @@ def main():
         elif a.perturb == "gradnoise":
             runners[f"grad_noise{run}"] = ingp_psnr.OracleRunner(
                 o, opt, grad_noise=(a.noise, 100 + run))
+        elif a.perturb == "acc":
+            # equally valid summation orders of the sums before each f16 rounding
+            # (oracle/ref_ingp.py acc=): f32 in BLAS order, f32 reversed (f64 = unperturbed)
+            arm = ("f32", "f32rev", "f32")[run] if run < 3 else None
+            if arm and f"acc_{arm}" not in runners:
+                o = ref_ingp.RefInstantNGP(cfg, state, ref_ingp.prep_kwargs(pp), p.scale,
+                                           scene.max_i, half=True, semantics=a.semantics,
+                                           ref_acc=a.ref_acc, acc=arm)
+                runners[f"acc_{arm}"] = ingp_psnr.OracleRunner(o, opt)
         elif a.perturb == "f32master":
             if run == 0:
                 runners["f32_master"] = ingp_psnr.OracleRunner(o, opt, master="f32")

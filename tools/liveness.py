@@ -64,11 +64,12 @@ def main():
         loss.backward()
         gz = (tab.grad != 0).float().mean().item()
         dz = (pipe._last_d_enc != 0).float().mean().item()
+        dr = (pipe._last_d_enc != 0).any(1).float().mean().item()
         sig = res["sigma_fine"]
         col = res["color_fine"]
         print(f"step {k:3d} loss {loss.item():.5f} sigma>0 {(sig > 0).float().mean().item():.4f} "
               f"color>0 {(col > 0).float().mean().item():.4f} table-grad nonzero {gz:.4f} "
-              f"dL/denc nonzero {dz:.4f} "
+              f"dL/denc nonzero {dz:.4f} rows {dr:.4f} "
               f"pred mean {res['color_map_fine'].float().mean().item():.4f} "
               f"target mean {batch['rad'].float().mean().item():.4f}", flush=True)
         opt.step()

@@ -161,6 +161,10 @@ _SIGNATURES = {
         [POINTER(HashGridDesc), _P, c_int64, c_int64, c_int64, _P, c_int32, _P, c_int32,
          c_int64, _P],
     ),
+    "anr_hashgrid_fwd_planes": (
+        c_int32,
+        [POINTER(HashGridDesc), _P, c_int64, c_int64, _P, c_int32, _P, c_int64, _P],
+    ),
     "anr_hashgrid_bwd": (
         c_int32,
         [POINTER(HashGridDesc), _P, c_int64, c_int64, _P, c_int32, c_int64, _P, _P],

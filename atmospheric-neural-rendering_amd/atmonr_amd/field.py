@@ -30,6 +30,7 @@ torch's caching allocator, at anr_ingp_field_bwd_workspace_bytes.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -65,15 +66,27 @@ class IngpFieldFn(torch.autograd.Function):
         t_hash = _lib.compute_copy(p_hash, enc_mod.dtype)
         dirs = dirs.float().contiguous()
 
-        enc = torch.empty(M, grid.n_out, device=dev, dtype=enc_mod.dtype)
-        call("anr_hashgrid_fwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(t_hash),
-             dtype_code(t_hash.dtype), ptr(enc), dtype_code(enc.dtype), enc.stride(0), s,
-             tag="hash_fwd")
+        fused = field_fused(pipe) and enc_mod.dtype == torch.float16
+        if fused and _enc_planes(grid):
+            # level-quad planes (anr_hashgrid_fwd_planes: one lane per sample, coalesced;
+            # 0.47-0.50 ms vs the row-layout walker's 0.63 at the bench shape), handed to the
+            # field kernels as enc_stride = -plane
+            nq = (grid.desc.n_levels + 3) // 4
+            enc = torch.empty(nq, M, 8, device=dev, dtype=torch.float16)
+            enc_ld = -8 * M
+            call("anr_hashgrid_fwd_planes", ctypes.byref(grid.desc), ptr(coords), 3, M,
+                 ptr(t_hash), dtype_code(t_hash.dtype), ptr(enc), 8 * M, s, tag="hash_fwd")
+        else:
+            enc = torch.empty(M, grid.n_out, device=dev, dtype=enc_mod.dtype)
+            enc_ld = enc.stride(0)
+            call("anr_hashgrid_fwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(t_hash),
+                 dtype_code(t_hash.dtype), ptr(enc), dtype_code(enc.dtype), enc_ld, s,
+                 tag="hash_fwd")
         ctx.pipe = pipe
         ctx.n_per_ray = n_per_ray
         ctx.params = (p_hash, p_pos, p_dir)
         ctx.rows = rows
-        fused = field_fused(pipe) and enc.dtype == torch.float16
+        ctx.enc_ld = enc_ld
         if rows is not None and not fused:
             raise _lib.ANRError("occupancy culling needs the fused f16 field")
         if cdt == torch.bfloat16 and not fused:
@@ -90,14 +103,14 @@ class IngpFieldFn(torch.autograd.Function):
             if rows is None:
                 sigma = torch.empty(M, device=dev, dtype=torch.float32)
                 color = torch.empty(M, nb, device=dev, dtype=torch.float32)
-                call("anr_ingp_field_fwd", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc.stride(0),
+                call("anr_ingp_field_fwd", pdesc, ddesc, mma, ptr(packed), ptr(enc), enc_ld,
                      ptr(dirs), n_per_ray, M, ptr(sigma), ptr(color), color.stride(0), s,
                      tag="field_fwd")
             else:
                 sigma = torch.zeros(m_dense, device=dev, dtype=torch.float32)
                 color = torch.zeros(m_dense, nb, device=dev, dtype=torch.float32)
                 call("anr_ingp_field_fwd_rows", pdesc, ddesc, mma, ptr(packed), ptr(enc),
-                     enc.stride(0), ptr(dirs), n_per_ray, M, ptr(rows), ptr(sigma), ptr(color),
+                     enc_ld, ptr(dirs), n_per_ray, M, ptr(rows), ptr(sigma), ptr(color),
                      color.stride(0), s, tag="field_fwd")
             ctx.fused_field = True
             ctx.save_for_backward(coords, dirs, enc, packed)
@@ -142,7 +155,7 @@ class IngpFieldFn(torch.autograd.Function):
              ptr(pos_out), pos_out.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(d_color),
              d_color.stride(0), ptr(d_sigma), ptr(d_pos_out), d_pos_out.stride(0), ptr(g_dir),
              s, tag="dir_mlp_bwd")
-        d_enc = torch.empty(M, enc.shape[1], device=dev, dtype=torch.float32)
+        d_enc = torch.empty(M, pipe.pos_encoder.hash_grids[0].n_out, device=dev, dtype=torch.float32)
         call("anr_mlp_bwd", ctypes.byref(pos_mod.desc), prec, ptr(w_pos), ptr(enc),
              dtype_code(enc.dtype), enc.stride(0), M, ptr(d_pos_out), _lib.F32,
              d_pos_out.stride(0), ptr(d_enc), _lib.F32, d_enc.stride(0), ptr(g_pos), s,
@@ -169,7 +182,7 @@ class IngpFieldFn(torch.autograd.Function):
             d_color = torch.zeros(M, pipe.dir_mlp.n_output_dims, device=dev)
         d_color = d_color.float().contiguous()
         d_sigma = d_sigma.float().contiguous() if d_sigma is not None else None
-        d_enc = torch.empty(M, enc.shape[1], device=dev, dtype=torch.float32)
+        d_enc = torch.empty(M, pipe.pos_encoder.hash_grids[0].n_out, device=dev, dtype=torch.float32)
         pdesc, ddesc = ctypes.byref(pipe.pos_mlp.desc), ctypes.byref(pipe.dir_mlp.desc)
         mma = _mma_code(pipe)
         ls = getattr(pipe, "loss_scale", None)
@@ -177,7 +190,7 @@ class IngpFieldFn(torch.autograd.Function):
             # reference numerics: tcnn's loss-scaled f16 backward (anr_ingp_field_bwd_ref16)
             if ctx.rows is not None:
                 raise _lib.ANRError("reference numerics: no occupancy culling")
-            call("anr_ingp_field_bwd_ref16", pdesc, ddesc, ptr(packed), ptr(enc), enc.stride(0),
+            call("anr_ingp_field_bwd_ref16", pdesc, ddesc, ptr(packed), ptr(enc), ctx.enc_ld,
                  ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color), d_color.stride(0),
                  ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), float(ls), s,
                  tag="field_bwd")
@@ -186,12 +199,12 @@ class IngpFieldFn(torch.autograd.Function):
             ws = torch.empty(max(1, -(-ws_bytes // 4)), device=dev, dtype=torch.float32)
             if ctx.rows is None:
                 call("anr_ingp_field_bwd", pdesc, ddesc, mma, ptr(packed), ptr(enc),
-                     enc.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
+                     ctx.enc_ld, ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
                      d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
                      ptr(ws), ws_bytes, s, tag="field_bwd")
             else:  # dL/d(sigma, color) are dense; read at the kept samples' rows
                 call("anr_ingp_field_bwd_rows", pdesc, ddesc, mma, ptr(packed), ptr(enc),
-                     enc.stride(0), ptr(dirs), ctx.n_per_ray, M, ptr(ctx.rows), ptr(d_sigma),
+                     ctx.enc_ld, ptr(dirs), ctx.n_per_ray, M, ptr(ctx.rows), ptr(d_sigma),
                      ptr(d_color), d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos),
                      ptr(g_dir), ptr(ws), ws_bytes, s, tag="field_bwd")
         _done(direct_p, p_pos, direct_d, p_dir)  # MLP grads final: their all-reduce may start
@@ -210,6 +223,16 @@ class IngpFieldFn(torch.autograd.Function):
 
 def _mma_code(pipe) -> int:
     return _lib.BF16 if pipe.pos_mlp.dtype == torch.bfloat16 else _lib.F16
+
+
+def _enc_planes(grid) -> bool:
+    """The fused field reads the hash features as level-quad planes (default) or, with
+    ANR_ENC_PLANES=0 (A/B), in the row layout of the walker forward."""
+    d = grid.desc
+    return (_ENC_PLANES and d.n_features == 2 and d.n_levels <= 16 and d.n_dims == 3)
+
+
+_ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"
 
 
 def field_fused(pipe) -> bool:

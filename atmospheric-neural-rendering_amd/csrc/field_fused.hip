@@ -250,7 +250,11 @@ __global__ void pack_kernel(const float* __restrict__ pp, const float* __restric
 struct Args {
   const _Float16* packed;
   const _Float16* enc;
+  // row r, levels 4g..4g+3 (one lane's 8 values) at enc + r * enc_stride + g * enc_gstride:
+  // row layout (M, >= 32): gstride 8; level-quad planes (anr_hashgrid_fwd_planes,
+  // enc_stride = -plane at the ABI): enc_stride 8, gstride = plane
   int64_t enc_stride;
+  int64_t enc_gstride;
   const float* dirs;
   uint32_t n_per_ray;
   int64_t M;
@@ -334,6 +338,29 @@ __device__ __forceinline__ h4 mask_h4(f4 g, h4 act) {
   return __builtin_bit_cast(h4, u2{m0, m1});
 }
 
+// Reference numerics: the gradient tiles hold tcnn's loss-scaled f16 values, many of them
+// deep in f16's subnormal range, and v_mfma_f32_16x16x32_f16 sums products of deeply
+// subnormal f16 operands inexactly (a single product is exact; 64-term sums of operands
+// ~2^-20 come out 28,844 f32 ulps rms from the exact sum against 62 for an f32 loop, with
+// a bias toward zero: tools/r5/mfma_precision.py, profiles/r05_mfma_precision.log). The
+// input-gradient products therefore take the subnormal part of the gradient operand
+// separately, scaled by 2^10 into the normal range (exact: a power of two, and every
+// subnormal times 2^10 stays below 1/16): W g = W g_normal + 2^-10 W (2^10 g_subnormal).
+// The split is exact and the two f32 partial sums are added once. (The dW products keep
+// the plain operand: their sums are dominated by the normal-range gradients.)
+#ifndef ANR_REF_SPLIT
+#define ANR_REF_SPLIT 1
+#endif
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split_sub(h4 g, h4& gn, h4& gs) {
+  const u16x4 b = __builtin_bit_cast(u16x4, g);
+  const u16x4 z = {0, 0, 0, 0};
+  const u16x4 sub = (b & u16x4{0x7C00, 0x7C00, 0x7C00, 0x7C00}) == z ? b : z;  // exp field 0
+  gn = __builtin_bit_cast(h4, b ^ sub);
+  const _Float16 k = static_cast<_Float16>(1024.0f);
+  gs = __builtin_bit_cast(h4, sub) * h4{k, k, k, k};
+}
+
 // Global inputs of one 16-sample half-tile for this lane, loaded a tile ahead.
 struct Rows {
   h8 xe;          // enc[row][8g .. 8g+7]
@@ -349,7 +376,7 @@ __device__ __forceinline__ void load_rows(const Args& a, int64_t row, int g, boo
   in.dc = f4{0.0f, 0.0f, 0.0f, 0.0f};
   in.ds = 0.0f;
   if (row >= a.M) return;
-  in.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+  in.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + g * a.enc_gstride);
   const int64_t drow = dense_row<ROWS>(a, row);
   if (g == 0) {
     const uint32_t ray = static_cast<uint32_t>(drow) / a.n_per_ray;
@@ -539,7 +566,7 @@ struct FwdRaw {
 
 template <bool ROWS>
 __device__ __forceinline__ void load_fwd_raw(const Args& a, int64_t row, int g, FwdRaw& r) {
-  r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+  r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + g * a.enc_gstride);
   const uint32_t ray = static_cast<uint32_t>(dense_row<ROWS>(a, row)) / a.n_per_ray;
   const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
   r.d0 = d[0];
@@ -618,7 +645,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) f
     const __amdgpu_buffer_rsrc_t rcol = out_rsrc(a.color, a.M * a.color_stride * 4);
     const uint32_t cs_bytes = static_cast<uint32_t>(a.color_stride) * 4u;
     auto enc_ptr = [&](int64_t t) {
-      return reinterpret_cast<const h8*>(a.enc + (t * 16 + li) * a.enc_stride + 8 * g);
+      return reinterpret_cast<const h8*>(a.enc + (t * 16 + li) * a.enc_stride + g * a.enc_gstride);
     };
     h8 nxe;
     if (tile < n_full) {
@@ -727,7 +754,7 @@ __global__ void __launch_bounds__(256) density_kernel(Args a) {
   int64_t tile = static_cast<int64_t>(blockIdx.x) * waves + wave;
   auto load = [&](int64_t t) -> h8 {
     const int64_t row = t * 16 + li;
-    if (row < a.M) return *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+    if (row < a.M) return *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + g * a.enc_gstride);
     return h8{};
   };
   h8 nxe = tile < n_tiles ? load(tile) : h8{};
@@ -817,7 +844,7 @@ struct RawRows {
 
 template <bool ROWS>
 __device__ __forceinline__ void load_raw(const Args& a, int64_t row, int g, RawRows& r) {
-  r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + 8 * g);
+  r.xe = *reinterpret_cast<const h8*>(a.enc + row * a.enc_stride + g * a.enc_gstride);
   const int64_t drow = dense_row<ROWS>(a, row);
   const uint32_t ray = static_cast<uint32_t>(drow) / a.n_per_ray;
   const float* d = a.dirs + static_cast<int64_t>(ray) * 3;
@@ -957,6 +984,36 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   }
   // f32 -> f16 -> f32 (the reference's f16 tensors between modules)
   auto r16 = [](float v) { return static_cast<float>(static_cast<_Float16>(v)); };
+  // input-gradient products (REF: subnormal part of the gradient operand split off, see
+  // split_sub); dx32 accumulates the K blocks of one product into (acc, accs), dx_join
+  // adds the two partial sums
+  constexpr bool SPLIT = REF && ANR_REF_SPLIT;
+  auto dx16 = [&](h4 w, h4 gg) -> f4 {
+    if constexpr (SPLIT) {
+      h4 gn, gs;
+      split_sub(gg, gn, gs);
+      return mma16<BF>(w, gn, z4) + mma16<BF>(w, gs, z4) * 0x1p-10f;
+    } else {
+      return mma16<BF>(w, gg, z4);
+    }
+  };
+  auto dx32 = [&](h8 w, h4 g0, h4 g1, f4& acc, f4& accs) {
+    if constexpr (SPLIT) {
+      h4 n0, s0, n1, s1;
+      split_sub(g0, n0, s0);
+      split_sub(g1, n1, s1);
+      acc = mma32<BF>(w, cat(n0, n1), acc);
+      accs = mma32<BF>(w, cat(s0, s1), accs);
+    } else {
+      acc = mma32<BF>(w, cat(g0, g1), acc);
+    }
+  };
+  auto dx_join = [&](f4 (&acc)[MT], const f4 (&accs)[MT]) {
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] += accs[mt] * 0x1p-10f;
+    }
+  };
 
   Rows cur[MT];
   // the next tile's raw inputs, loaded a tile ahead into alternating register sets (the
@@ -1056,7 +1113,7 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
           mma32_acc_v<BF>(dD2[kt], ga[pr], xl);
         }
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) dl[mt][kt] = mask_h4<BF>(mma16<BF>(wd2[kt], gc[mt], z4), last(mt, kt));
+        for (int mt = 0; mt < MT; ++mt) dl[mt][kt] = mask_h4<BF>(dx16(wd2[kt], gc[mt]), last(mt, kt));
       }
     }
     // ---- dir hidden layer 1 (NHD == 2): dW_D1 (W x W) += dl^T · X_d0 ; dh0 = D1^T dl
@@ -1081,15 +1138,16 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       }
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
-        f4 acc[MT];
+        f4 acc[MT], accs[MT];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = accs[mt] = z4;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc[mt] = mma32<BF>(wd1[kt * KB + kb], cat(dl[mt][2 * kb], dl[mt][2 * kb + 1]), acc[mt]);
+            dx32(wd1[kt * KB + kb], dl[mt][2 * kb], dl[mt][2 * kb + 1], acc[mt], accs[mt]);
         }
+        dx_join(acc, accs);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) dh0[mt][kt] = mask_h4<BF>(acc[mt], t[mt].hd0[kt]);
       }
@@ -1119,14 +1177,15 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
           mma32_acc_v<BF>(dD0[nt * 2 + 1], gd, x1);
         }
       }
-      f4 acc[MT];
+      f4 acc[MT], accs[MT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = accs[mt] = z4;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = mma32<BF>(wd0[kb], cat(dh0[mt][2 * kb], dh0[mt][2 * kb + 1]), acc[mt]);
+        for (int mt = 0; mt < MT; ++mt) dx32(wd0[kb], dh0[mt][2 * kb], dh0[mt][2 * kb + 1], acc[mt], accs[mt]);
       }
+      dx_join(acc, accs);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         if constexpr (REF) {
@@ -1158,7 +1217,7 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
           mma32_acc_v<BF>(dP1[kt], ga[pr], xp);
         }
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) dhp[mt][kt] = mask_h4<BF>(mma16<BF>(wp1[kt], dpo[mt], z4), t[mt].hp[kt]);
+        for (int mt = 0; mt < MT; ++mt) dhp[mt][kt] = mask_h4<BF>(dx16(wp1[kt], dpo[mt]), t[mt].hp[kt]);
       }
     }
     // ---- pos input layer: dW_P0 (W x 32) += dhp^T · X_pe ; d_enc = P0^T dhp
@@ -1182,15 +1241,16 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       }
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        f4 acc[MT];
+        f4 acc[MT], accs[MT];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = z4;
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = accs[mt] = z4;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc[mt] = mma32<BF>(wp0[kt * KB + kb], cat(dhp[mt][2 * kb], dhp[mt][2 * kb + 1]), acc[mt]);
+            dx32(wp0[kt * KB + kb], dhp[mt][2 * kb], dhp[mt][2 * kb + 1], acc[mt], accs[mt]);
         }
+        dx_join(acc, accs);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int64_t row = tile * TR + mt * 16 + li;
@@ -1486,6 +1546,23 @@ extern "C" int anr_ingp_field_set_grad_scale(int32_t log2_target) {
 
 static bool mma_ok(int32_t t) { return t == ANR_F16 || t == ANR_BF16; }
 
+// enc_stride >= 32 (multiple of 8): row layout; enc_stride = -P: level-quad planes of P
+// f16 elements each (P >= 8 M, multiple of 8), as anr_hashgrid_fwd_planes writes them
+static bool set_enc(Args& a, const void* enc, int64_t enc_stride, int64_t M) {
+  a.enc = static_cast<const _Float16*>(enc);
+  if (enc_stride >= 32 && enc_stride % 8 == 0) {
+    a.enc_stride = enc_stride;
+    a.enc_gstride = 8;
+    return true;
+  }
+  if (enc_stride < 0 && -enc_stride >= 8 * M && (-enc_stride) % 8 == 0) {
+    a.enc_stride = 8;
+    a.enc_gstride = -enc_stride;
+    return true;
+  }
+  return false;
+}
+
 extern "C" int anr_ingp_field_pack(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
                                    int32_t mma_dtype, const float* pos_params,
                                    const float* dir_params, void* packed, anr_stream_t stream) {
@@ -1516,16 +1593,16 @@ static int field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_fwd: bad M");
   if (M == 0) return ANR_OK;
   ANR_CHECK_ARG(packed && enc && dirs && sigma && color, "anr_ingp_field_fwd: null pointer");
-  ANR_CHECK_ARG(n_per_ray >= 1 && n_per_ray < (1LL << 31) && enc_stride >= 32 &&
-                    enc_stride % 8 == 0 && color_stride >= dir->n_output,
+  ANR_CHECK_ARG(n_per_ray >= 1 && n_per_ray < (1LL << 31) && color_stride >= dir->n_output,
                 "anr_ingp_field_fwd: bad shape/stride");
   ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(enc) & 15) == 0 &&
                     (reinterpret_cast<uintptr_t>(packed) & 15) == 0,
                 "anr_ingp_field_fwd: enc/packed must be 16-byte aligned");
   Args a{};
   a.packed = static_cast<const _Float16*>(packed);
-  a.enc = static_cast<const _Float16*>(enc);
-  a.enc_stride = enc_stride;
+  ANR_CHECK_ARG(set_enc(a, enc, enc_stride, M),
+                "anr_ingp_field: bad enc_stride %lld (>= 32, multiple of 8: rows; -P: level-quad "
+                "planes of P >= 8 M)", (long long)enc_stride);
   a.dirs = dirs;
   a.n_per_ray = static_cast<uint32_t>(n_per_ray);
   a.M = M;
@@ -1556,8 +1633,7 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   if (M == 0) return ANR_OK;
   ANR_CHECK_ARG(packed && enc && dirs && d_color && d_enc && g_pos && g_dir,
                 "anr_ingp_field_bwd: null pointer");
-  ANR_CHECK_ARG(n_per_ray >= 1 && n_per_ray < (1LL << 31) && enc_stride >= 32 &&
-                    enc_stride % 8 == 0 && d_color_stride >= dir->n_output &&
+  ANR_CHECK_ARG(n_per_ray >= 1 && n_per_ray < (1LL << 31) && d_color_stride >= dir->n_output &&
                     d_enc_stride >= 32 && d_enc_stride % 4 == 0,
                 "anr_ingp_field_bwd: bad shape/stride");
   ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(enc) & 15) == 0 &&
@@ -1566,8 +1642,9 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
                 "anr_ingp_field_bwd: enc/packed/d_enc must be 16-byte aligned");
   Args a{};
   a.packed = static_cast<const _Float16*>(packed);
-  a.enc = static_cast<const _Float16*>(enc);
-  a.enc_stride = enc_stride;
+  ANR_CHECK_ARG(set_enc(a, enc, enc_stride, M),
+                "anr_ingp_field: bad enc_stride %lld (>= 32, multiple of 8: rows; -P: level-quad "
+                "planes of P >= 8 M)", (long long)enc_stride);
   a.dirs = dirs;
   a.n_per_ray = static_cast<uint32_t>(n_per_ray);
   a.M = M;
@@ -1610,14 +1687,13 @@ extern "C" int anr_ingp_field_density(const anr_mlp_desc* pos, const anr_mlp_des
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_density: bad M");
   if (M == 0) return ANR_OK;
   ANR_CHECK_ARG(packed && enc && sigma, "anr_ingp_field_density: null pointer");
-  ANR_CHECK_ARG(enc_stride >= 32 && enc_stride % 8 == 0, "anr_ingp_field_density: bad stride");
+
   ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(enc) & 15) == 0 &&
                     (reinterpret_cast<uintptr_t>(packed) & 15) == 0,
                 "anr_ingp_field_density: enc/packed must be 16-byte aligned");
   Args a{};
   a.packed = static_cast<const _Float16*>(packed);
-  a.enc = static_cast<const _Float16*>(enc);
-  a.enc_stride = enc_stride;
+  ANR_CHECK_ARG(set_enc(a, enc, enc_stride, M), "anr_ingp_field_density: bad enc_stride");
   a.M = M;
   a.sigma = sigma;
   ANR_CHECK_ARG(dispatch(v, mma_dtype == ANR_BF16, 3, a, nullptr, 0,

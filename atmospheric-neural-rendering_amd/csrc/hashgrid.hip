@@ -655,6 +655,115 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v6_kernel(
       os_bytes);
 }
 
+// ---------------------------------------------------------------------------------------
+// Forward v9 "quad planes" (F = 2, f16 output): one lane per SAMPLE, every level, output
+// in level-quad planes -- plane q holds levels 4q..4q+3 of every row, 16 B per row
+// (level l feature f of row m at out[(l / 4) * plane + 8 m + 2 (l % 4) + f]). The walkers
+// (v1 / v6) keep a lane on one level of one chunk and re-gather only on a cell change,
+// but their wavefronts touch 4-16 chunks far apart, so each gather instruction lands on as
+// many unrelated lines. Here a wavefront's 64 lanes are 64 consecutive samples of one
+// ray: a corner gather's addresses coincide wherever neighbouring samples share a cell
+// (all of them on the coarse levels, ~4 per cell on the finest), the coordinate load is
+// one contiguous 768 B, and each quad's store is one contiguous 1 KiB (a level-major row
+// layout written lane by lane leaves partial lines: 1.57 ms measured, against 0.47 for
+// the planes). Every sample gathers its 8 corners per level (no cell reuse inside a
+// lane). Same corner order, weights and fma chain as v6: bit-identical values. Measured
+// on the bench coordinates (profiles/r05_hash_fwd_planes.log): v6 0.634 ms, v9 0.47-0.50
+// ms; pinning level pairs to XCDs (block b -> XCD b % 8) made it slower (0.77 / 1.13 ms:
+// every XCD then reads every coordinate).
+template <int D, typename TT>
+__global__ void __launch_bounds__(256) hashgrid_fwd_planes_kernel(
+    GridLevels G, int n_levels, const float* __restrict__ x, uint32_t x_bytes, uint32_t xs4,
+    int64_t M, const TT* __restrict__ table, uint32_t table_bytes, __half* __restrict__ out,
+    uint32_t out_bytes, uint32_t plane_bytes) {
+  using R = Raw2<TT>;
+  const int64_t m = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rx = wave_rsrc(x, x_bytes);
+  const __amdgpu_buffer_rsrc_t rt = wave_rsrc(table, table_bytes);
+  const __amdgpu_buffer_rsrc_t ro = wave_rsrc(out, out_bytes);
+  const uint32_t xo = static_cast<uint32_t>(m) * xs4;  // past the end: loads return 0
+  float xv[D];
+  if constexpr (D == 3) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rx, xo, 0, 0);
+    xv[0] = __uint_as_float(v[0]);
+    xv[1] = __uint_as_float(v[1]);
+    xv[2] = __uint_as_float(v[2]);
+  } else {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rx, xo, 0, 0);
+    xv[0] = __uint_as_float(v[0]);
+    xv[1] = __uint_as_float(v[1]);
+  }
+  // rows past M: the stores are dropped by the range check (offset >= out_bytes)
+  const uint32_t orow = m < M ? static_cast<uint32_t>(m) * 16u : 0x80000000u;
+  const int n_quads = (n_levels + 3) >> 2;
+  for (int q = 0; q < n_quads; ++q) {
+    uint32_t packed[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int level = 4 * q + j;
+      packed[j] = 0u;  // a partial last quad is zero-filled
+      if (level >= n_levels) continue;  // wave-uniform
+      const float scale = G.scale[level];
+      const uint32_t res = G.res[level];
+      const uint32_t T = G.size[level];
+      const uint32_t base = G.offset[level] * R::bytes;
+      LevelIdx<D> li;
+      li.init(T, res);
+      const uint32_t hmask = T - 1u;
+      float w[D];
+      uint32_t g[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const float p = fmaf(scale, xv[d], 0.5f);
+        const float fl = floorf(p);
+        g[d] = static_cast<uint32_t>(static_cast<int>(fl));
+        w[d] = p - fl;
+      }
+      uint32_t comp[D][2];
+      li.dims(g, comp);
+      uint32_t idx[1 << D], sum[1 << D];
+#pragma unroll
+      for (int c = 0; c < (1 << D); ++c) {
+        uint32_t hx = 0u, sm = 0u;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          hx ^= comp[d][(c >> d) & 1];
+          sm += comp[d][(c >> d) & 1];
+        }
+        sum[c] = sm;
+        idx[c] = li.hashed ? (hx & hmask) : sm;
+      }
+      uint32_t gmax = g[0];
+#pragma unroll
+      for (int d = 1; d < D; ++d) gmax = gmax > g[d] ? gmax : g[d];
+      if (!li.hashed && gmax >= res - 1u) {
+#pragma unroll
+        for (int c = 0; c < (1 << D); ++c)
+          if (sum[c] >= T) {
+            const uint32_t s1 = sum[c] - T;
+            idx[c] = s1 < T ? s1 : sum[c] % T;
+          }
+      }
+      typename R::type val[1 << D];
+#pragma unroll
+      for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, base + idx[c] * R::bytes);
+      float a0 = 0.0f, a1 = 0.0f;
+#pragma unroll
+      for (int c = 0; c < (1 << D); ++c) {
+        float wt = 1.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
+        R::fma2(wt, val[c], a0, a1);
+      }
+      packed[j] = __builtin_bit_cast(uint32_t, __floats2half2_rn(a0, a1));
+    }
+    typedef uint32_t u4q __attribute__((vector_size(16)));
+    const u4q v = {packed[0], packed[1], packed[2], packed[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(v, ro, static_cast<uint32_t>(q) * plane_bytes + orow,
+                                           0, 0);
+  }
+}
+
 // XS / DS: compile-time coordinate and dL/dy row strides (0 = the run-time x_stride /
 // dout_stride). With both known (the fused field's (M,3) coordinates and (M,32) dL/denc)
 // every prefetch address is a per-batch scalar base plus immediate offsets: the walk
@@ -1217,6 +1326,52 @@ extern "C" int anr_hashgrid_fwd(const anr_hashgrid_desc* d, const float* x,
                                 int64_t out_stride, anr_stream_t stream) {
   return anr_hashgrid_fwd_runs(d, x, x_stride, M, 0, table, table_dtype, out, out_dtype,
                                out_stride, stream);
+}
+
+extern "C" int anr_hashgrid_fwd_planes(const anr_hashgrid_desc* d, const float* x,
+                                       int64_t x_stride, int64_t M, const void* table,
+                                       int32_t table_dtype, void* out, int64_t plane_stride,
+                                       anr_stream_t stream) {
+  using namespace anr;
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(d && x && table && out, "anr_hashgrid_fwd_planes: null argument");
+  ANR_CHECK_ARG(M > 0 && x_stride >= d->n_dims && plane_stride >= 8 * M,
+                "anr_hashgrid_fwd_planes: bad shape/stride (plane_stride >= 8 M)");
+  ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0 && (plane_stride & 7) == 0,
+                "anr_hashgrid_fwd_planes: out and plane_stride must be 16-byte aligned");
+  ANR_CHECK_ARG(table_dtype == ANR_F16 || table_dtype == ANR_F32,
+                "anr_hashgrid_fwd_planes: bad dtype");
+  ANR_CHECK_ARG(d->n_features == 2 && d->n_levels <= 16 && (d->n_dims == 2 || d->n_dims == 3),
+                "anr_hashgrid_fwd_planes: 2 features, <= 16 levels, 2-D or 3-D");
+  GridLevels G;
+  ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_fwd_planes: descriptor not initialised");
+  const int64_t esz_t = table_dtype == ANR_F16 ? 2 : 4;
+  const int64_t n_quads = (d->n_levels + 3) / 4;
+  const int64_t x_bytes = ((M - 1) * x_stride + d->n_dims) * 4;
+  const int64_t t_bytes =
+      static_cast<int64_t>(G.offset[d->n_levels - 1] + G.size[d->n_levels - 1]) * 2 * esz_t;
+  const int64_t o_bytes = ((n_quads - 1) * plane_stride + 8 * M) * 2;
+  const int64_t lim = int64_t(1) << 31;
+  ANR_CHECK_ARG(x_bytes < lim && t_bytes < lim && o_bytes < lim &&
+                    (M + 256) * x_stride * 4 < lim && plane_stride * 2 < lim,
+                "anr_hashgrid_fwd_planes: byte ranges must stay below 2^31");
+  const dim3 grid(static_cast<unsigned>(ceil_div(M, 256))), block(256);
+#define ANR_HG_PL(D_, TT)                                                                    \
+  hipLaunchKernelGGL((hashgrid_fwd_planes_kernel<D_, TT>), grid, block, 0, as_stream(stream), \
+                     G, d->n_levels, x, static_cast<uint32_t>(x_bytes),                      \
+                     static_cast<uint32_t>(x_stride * 4), M, static_cast<const TT*>(table),  \
+                     static_cast<uint32_t>(t_bytes), static_cast<__half*>(out),              \
+                     static_cast<uint32_t>(o_bytes), static_cast<uint32_t>(plane_stride * 2))
+  if (d->n_dims == 3) {
+    if (table_dtype == ANR_F16) ANR_HG_PL(3, __half);
+    else ANR_HG_PL(3, float);
+  } else {
+    if (table_dtype == ANR_F16) ANR_HG_PL(2, __half);
+    else ANR_HG_PL(2, float);
+  }
+#undef ANR_HG_PL
+  ANR_CHECK_LAUNCH("anr_hashgrid_fwd_planes");
+  return ANR_OK;
 }
 
 extern "C" int anr_hashgrid_bwd(const anr_hashgrid_desc* d, const float* x,

@@ -29,7 +29,9 @@
 extern "C" {
 #endif
 
-#define ANR_ABI_VERSION 2
+/* ABI 3 (r05): anr_hashgrid_fwd_planes, and the fused field entry points' enc_stride < 0
+ * selecting the level-quad-plane layout it writes. */
+#define ANR_ABI_VERSION 3
 
 enum anr_dtype { ANR_F32 = 0, ANR_F16 = 1, ANR_BF16 = 2 };
 
@@ -177,6 +179,17 @@ int anr_hashgrid_bwd_count_requests(const anr_hashgrid_desc* d, const float* x,
 /* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)
  * f32, ACCUMULATED (caller zeroes). Duplicate corner updates inside a wavefront are
  * pre-summed before the f32 atomics (samples along one ray share cells). */
+/* Level-quad-plane forward (r05; hashgrid.hip forward v9, one lane per sample): the same
+ * features as anr_hashgrid_fwd with f16 output, laid out as planes of four levels: level
+ * l, feature f of row m at out[(l / 4) * plane_stride + 8 m + 2 (l % 4) + f]
+ * (plane_stride >= 8 M f16 elements, multiple of 8; out 16-byte aligned; a partial last
+ * quad is zero-filled). 2 features, <= 16 levels. The fused field kernels read this
+ * layout when given enc_stride = -plane_stride. Replaces the same call site as
+ * anr_hashgrid_fwd (instant_ngp.py:163, the tcnn Encoding forward). */
+int anr_hashgrid_fwd_planes(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
+                            int64_t M, const void* table, int32_t table_dtype, void* out,
+                            int64_t plane_stride, anr_stream_t stream);
+
 int anr_hashgrid_bwd(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
                      int64_t M, const void* dout, int32_t dout_dtype, int64_t dout_stride,
                      float* dtable, anr_stream_t stream);
@@ -278,7 +291,10 @@ int anr_ingp_dir_mlp_bwd(const anr_mlp_desc* d, int32_t precision, const void* p
  * Weights: anr_ingp_field_pack converts the f32 master parameters of both networks
  * (tcnn layout) into one 16-bit buffer of anr_ingp_field_packed_size elements (MFMA
  * fragment order); run it after every optimizer step.
- * Forward: enc (M, >=32) f16 (16-byte aligned rows), dirs (M/n_per_ray, 3) f32 ->
+ * enc (every entry point below): f16 hash features, enc_stride >= 32 (multiple of 8) for
+ *   the row layout (M, enc_stride) with 16-byte aligned rows, or enc_stride = -P for the
+ *   level-quad planes of anr_hashgrid_fwd_planes (P >= 8 M, multiple of 8).
+ * Forward: enc, dirs (M/n_per_ray, 3) f32 ->
  *   sigma (M,) f32 = relu(pos_out[:,0]), color (M, n_output) f32 = relu(dir_mlp(...)).
  * Backward: d_sigma (M,) f32 (nullable), d_color (M, n_output) f32 -> d_enc (M, 32) f32
  *   WRITTEN; g_pos / g_dir f32 parameter gradients ACCUMULATED. `workspace` is caller-

@@ -1140,5 +1140,81 @@ def test_hashgrid_fwd_v6_outside_grid_and_strides(dev, cfg, M, xs, tdt):
                   _lib.stream(dev))
         lib.anr_hashgrid_force_v1(prev)
         outs.append(out)
-    assert torch.equal(outs[0], outs[1])
-    assert torch.all(outs[1][:, L * 2:] == -9) and torch.all(outs[1][M] == -9)
+    for o_ in outs[1:]:
+        assert torch.equal(outs[0], o_)
+        assert torch.all(o_[:, L * 2:] == -9) and torch.all(o_[M] == -9)
+    # the level-quad-plane entry point (v9, one lane per sample): the same values (f16
+    # output) with level l, feature f of row m at out[(l // 4) * plane + 8 m + 2 (l % 4) + f],
+    # a partial last quad zero-filled, nothing written past row M of a plane
+    plane = 8 * M + 16
+    nq = -(-L // 4)
+    pl = torch.full((nq * plane + 8,), -9.0, device=dev, dtype=torch.float16)
+    _lib.call("anr_hashgrid_fwd_planes", ctypes.byref(d), x.data_ptr(), xs, M,
+              table.data_ptr(), _lib.dtype_code(dt), pl.data_ptr(), plane, _lib.stream(dev))
+    got = torch.cat([pl[q * plane:q * plane + 8 * M].view(M, 8) for q in range(nq)], 1)
+    assert torch.equal(got[:, :2 * L], outs[0][:M, :2 * L].half())
+    assert torch.all(got[:, 2 * L:] == 0)
+    for q in range(nq):
+        assert torch.all(pl[q * plane + 8 * M:(q + 1) * plane] == -9)
+
+
+@pytest.mark.parametrize("mma,ref", [("f16", False), ("bf16", False), ("f16", True)])
+@pytest.mark.parametrize("n_per_ray,R,extra", [(1024, 5, 0), (64, 9, 13)])
+def test_ingp_field_enc_quad_planes_equal_rows(dev, mma, ref, n_per_ray, R, extra):
+    """The fused field reads its f16 hash features either in the row layout (M, 32) or in
+    the level-quad planes anr_hashgrid_fwd_planes writes (enc_stride = -plane): forward,
+    density, backward and the reference-numerics backward give bit-identical sigma /
+    colour / dL/denc, and parameter gradients equal up to the atomic flush order."""
+    from atmonr_amd import _lib
+
+    width, nhd, nb = 64, 2, 4
+    M = R * n_per_ray + extra
+    code = _lib.BF16 if mma == "bf16" else _lib.F16
+    g = torch.Generator(device=dev).manual_seed(21)
+    lib = _lib.load()
+    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
+    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
+    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
+    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
+    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
+    plane = 8 * M + 24
+    planes = torch.zeros(4 * plane, device=dev, dtype=torch.float16)
+    for q in range(4):
+        planes[q * plane:q * plane + 8 * M] = enc[:, 8 * q:8 * q + 8].reshape(-1)
+    dirs = torch.rand(R + 1, 3, device=dev, generator=g)
+    s = _lib.stream(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", pb, db, code, pp.data_ptr(), pd.data_ptr(),
+              packed.data_ptr(), s)
+    dcol = (torch.randn(M, nb, device=dev, generator=g) * 1e-2).half().float()
+    dsig = (torch.randn(M, device=dev, generator=g) * 1e-3).half().float()
+    ws_bytes = lib.anr_ingp_field_bwd_workspace_bytes(pb, db, code, M)
+    ws = torch.empty(max(1, ws_bytes // 4), device=dev)
+    out = {}
+    for name, base, ld in (("rows", enc, 32), ("planes", planes, -plane)):
+        sigma, color = torch.empty(M, device=dev), torch.empty(M, nb, device=dev)
+        _lib.call("anr_ingp_field_fwd", pb, db, code, packed.data_ptr(), base.data_ptr(), ld,
+                  dirs.data_ptr(), n_per_ray, M, sigma.data_ptr(), color.data_ptr(), nb, s)
+        dens = torch.empty(M, device=dev)
+        _lib.call("anr_ingp_field_density", pb, db, code, packed.data_ptr(), base.data_ptr(), ld,
+                  M, dens.data_ptr(), s)
+        d_enc = torch.empty(M, 32, device=dev)
+        g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
+        if ref:
+            _lib.call("anr_ingp_field_bwd_ref16", pb, db, packed.data_ptr(), base.data_ptr(), ld,
+                      dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), 128.0, s)
+        else:
+            _lib.call("anr_ingp_field_bwd", pb, db, code, packed.data_ptr(), base.data_ptr(), ld,
+                      dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(),
+                      ws.data_ptr() if ws_bytes else None, ws_bytes, s)
+        out[name] = (sigma, color, dens, d_enc, g_pos, g_dir)
+    for a, b in zip(out["rows"][:4], out["planes"][:4]):
+        assert torch.equal(a, b)
+    for a, b in zip(out["rows"][4:], out["planes"][4:]):
+        assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item()
+    with pytest.raises(_lib.ANRError):  # a plane shorter than 8 M rows is refused
+        _lib.call("anr_ingp_field_fwd", pb, db, code, packed.data_ptr(), planes.data_ptr(),
+                  -(8 * M - 8), dirs.data_ptr(), n_per_ray, M, sigma.data_ptr(),
+                  color.data_ptr(), nb, s)

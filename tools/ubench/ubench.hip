@@ -176,6 +176,30 @@ __global__ void f16_denorm_kernel(float* out) {
   }
 }
 
+// MFMA accumulation precision (r05 PSNR-drift probe): n_mats independent products
+// C = A0 B0 + A1 B1 (two chained v_mfma_f32_16x16x32_f16, the field backward's K = 64
+// input-gradient shape). Operands in the instruction's register layout: lane l holds
+// A[row l % 16][k = 8 (l / 16) .. + 7] and B[k = 8 (l / 16) .. + 7][col l % 16]; C lane l
+// row 4 (l / 16) + i, col l % 16. a, b: n_mats * 2 * 64 * 8 halves (lane-linear); c:
+// n_mats * 64 * 4 floats.
+__global__ void mfma_dot_kernel(const _Float16* __restrict__ a, const _Float16* __restrict__ b,
+                                float* __restrict__ c, int n_mats) {
+  const int l = threadIdx.x & 63;
+  const int mat = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (mat >= n_mats) return;
+  ub_f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int kb = 0; kb < 2; ++kb) {
+    const int64_t o = ((static_cast<int64_t>(mat) * 2 + kb) * 64 + l) * 8;
+    ub_h8 av, bv;
+    for (int e = 0; e < 8; ++e) {
+      av[e] = a[o + e];
+      bv[e] = b[o + e];
+    }
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
+  }
+  for (int i = 0; i < 4; ++i) c[(static_cast<int64_t>(mat) * 64 + l) * 4 + i] = acc[i];
+}
+
 extern "C" {
 
 int ub_xcc_map(void* out, int blocks, int spin, void* stream) {
@@ -226,6 +250,13 @@ int ub_gather(const void* table, int64_t n_words, int iters, int blocks, uint32_
   if (n_words <= 0 || iters <= 0 || blocks <= 0) return 1;
   gather_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((const uint32_t*)table, n_words, iters,
                                                          seed, (uint32_t*)sink);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int ub_mfma_dot(const void* a, const void* b, float* c, int n_mats, void* stream) {
+  if (n_mats <= 0) return 1;
+  mfma_dot_kernel<<<(n_mats + 3) / 4, 256, 0, (hipStream_t)stream>>>(
+      (const _Float16*)a, (const _Float16*)b, c, n_mats);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -349,7 +349,7 @@ __device__ __forceinline__ h4 mask_h4(f4 g, h4 act) {
 // The split is exact and the two f32 partial sums are added once. (The dW products keep
 // the plain operand: their sums are dominated by the normal-range gradients.)
 #ifndef ANR_REF_SPLIT
-#define ANR_REF_SPLIT 1
+#define ANR_REF_SPLIT 0
 #endif
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void split_sub(h4 g, h4& gn, h4& gs) {

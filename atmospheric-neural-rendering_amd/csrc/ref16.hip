@@ -29,7 +29,18 @@ namespace ref16 {
 constexpr int kMaxC = 8;
 constexpr int kSeg = 64;   // samples per ray and segment: one per lane
 
-__device__ __forceinline__ float h(float x) { return __half2float(__float2half_rn(x)); }
+// Round an f32 VALUE to f16. The asm barrier makes the f32 rounding of the expression that
+// produced x happen first: without it the backend fuses h(a * b) and h(a + b) into one
+// v_fma_mixlo_f16, which rounds the EXACT product / sum to f16 once, where torch's f16 ops
+// round to f32 (opmath) and then to f16. The two differ when the f32 result lands on an f16
+// tie (z_vals * scale -> f16 km, x * (1 / max_i), norm * d, gt + eps): measured on the
+// PSNR test's first step, 6 of 65,536 dL/dsigma moved between neighbouring samples (an f16
+// z one ulp off shifts a mid-point, i.e. swaps two deltas) -- the r04 N = 1,024 PSNR drift
+// (tools/r5/composite_ref16_diag.py).
+__device__ __forceinline__ float h(float x) {
+  asm("" : "+v"(x));
+  return __half2float(__float2half_rn(x));
+}
 
 // f64 -> f16 with ONE rounding (round to odd into f32, then nearest-even into f16: the
 // f32 intermediate has 13 more bits than f16, so the double rounding is exact)

@@ -25,6 +25,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "atmospheric-neural-rendering_amd")]
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
@@ -35,6 +36,18 @@ def compare(g, r):
             "sign_mismatch": int(((g > 0) & (r < 0)).sum() + ((g < 0) & (r > 0)).sum()),
             "nonzero_ref": int((r != 0).sum()), "n": int(r.numel()),
             "equal_frac": float((g == r).double().mean())}
+
+
+def table_detail(g_gpu, g64, g32, offsets, top=8):
+    """The largest |gpu - f64| entries of the hash-table gradient: level, value triple."""
+    d = (g_gpu - g64).abs()
+    idx = torch.topk(d, top).indices
+    out = []
+    for e in idx.tolist():
+        lvl = int(np.searchsorted(offsets * 2, e, side="right") - 1)
+        out.append({"entry": e, "level": lvl, "f64": float(g64[e]), "f32": float(g32[e]),
+                    "gpu": float(g_gpu[e])})
+    return out
 
 
 def main():
@@ -67,8 +80,30 @@ def main():
         return ref_ingp.RefInstantNGP(cfg, state0, ref_ingp.prep_kwargs(pp), p.scale,
                                       scene.max_i, half=True, semantics="reference", acc=acc)
 
+    from oracle import ref_tcnn
+
+    offsets = ref_tcnn.grid_levels(3, 16, 16, 1.3819, int(cfg["instant_ngp"]["encoding"]["log2_hashmap_size"]))[0]
+    captured = {}
+    orig = ref_ingp._TcnnCall.apply
+
+    def spy(x, params, fn, *rest):
+        y = orig(x, params, fn, *rest)
+        for tag, o_ in (("enc", o64), ("enc32", o32)):
+            if params is o_.params["pos_encoder"] and y.requires_grad:
+                y.retain_grad()
+                captured[tag] = y
+        if params is o64.params["pos_mlp"] and y.requires_grad:
+            y.retain_grad()
+            captured["pos_out"] = y
+        if params is o64.params["dir_mlp"] and y.requires_grad:
+            y.retain_grad()
+            captured["dir_out"] = y
+        return y
+    ref_ingp._TcnnCall.apply = spy
+    p._keep_d_enc = True
     o64 = oracle("f64")
     o32 = oracle("f32")
+    ref_ingp._TcnnCall.apply = spy
     opt = o64.optimizer(opt_cfg)
     cps = sorted(int(c) for c in a.checkpoints.split(","))
     gen = torch.Generator().manual_seed(ingp_psnr.SEED_U)
@@ -108,6 +143,10 @@ def main():
         if it in cps:
             row["loss"] = {"f64": float(l64), "f32": float(o32.loss(cb, r32).detach()),
                            "gpu": float(lg)}
+            for key in ("sigma_fine", "color_fine"):
+                a64 = r64[key].detach().double().reshape(-1)
+                row[key] = {"f32": compare(r32[key].detach().double().reshape(-1), a64),
+                            "gpu": compare(rg[key].detach().double().cpu().reshape(-1), a64)}
             cm64 = r64["color_map_fine"].detach().double()
             row["color_map"] = {
                 "f32": compare(r32["color_map_fine"].detach().double(), cm64),
@@ -116,6 +155,60 @@ def main():
                 g64 = o64.params[m].grad.detach()
                 row[m] = {"f32": compare(o32.params[m].grad.detach(), g64),
                           "gpu": compare(getattr(p, m).params.grad.detach().double().cpu(), g64)}
+            g_gpu = p.pos_encoder.params.grad.detach().double().cpu()
+            g64 = o64.params["pos_encoder"].grad.detach()
+            row["table_top"] = table_detail(g_gpu, g64, o32.params["pos_encoder"].grad.detach(),
+                                            offsets)
+            # the sample coordinates the GPU walked vs the oracle's (f64 libm differences
+            # of the preprocessor move them by ulps; near a cell face that changes the cell)
+            from oracle import ref_path, ref_nerf
+            pts, _ = ref_path.sample_uniform_bins(cb["origin"], cb["dir"], cb["len"], u=u,
+                                                  n_bins=a.samples)
+            pts = (ref_nerf.preprocess_torch(pts, **o64.prep) + 1) / 2
+            pts = torch.cat([pts[..., :2], pts[..., 2:] / o64.alt], -1).float().reshape(-1, 3)
+            xg = p._last_hash_bwd[0].cpu()
+            row["coords"] = {"differ_frac": float((xg != pts).any(1).double().mean()),
+                             "max_abs": float((xg - pts).abs().max())}
+            if "enc" in captured and getattr(p, "_last_d_enc", None) is not None:
+                de_o = captured["enc"].grad.double()
+                de_g = p._last_d_enc.double().cpu()
+                row["d_enc"] = {"rows_differ_frac": float((de_o != de_g).any(1).double().mean()),
+                                "elems_differ_frac": float((de_o != de_g).double().mean()),
+                                "zero_flips": int(((de_o == 0) != (de_g == 0)).sum()),
+                                "rel_l2": float((de_o - de_g).norm() / de_o.norm())}
+                if "enc32" in captured:
+                    de_3 = captured["enc32"].grad.double()
+                    row["d_enc_f32arm"] = {
+                        "rows_differ_frac": float((de_o != de_3).any(1).double().mean()),
+                        "rel_l2": float((de_o - de_3).norm() / de_o.norm())}
+                ds_g, dc_g = (t_.double().cpu() for t_ in p._last_field_grads)
+                po_g = captured["pos_out"].grad.double()
+                pos_out = captured["pos_out"].detach().double()
+                ds_o = torch.where(pos_out[:, 0] > 0, po_g[:, 0], torch.zeros_like(po_g[:, 0]))
+                live = pos_out[:, 0] > 0
+                ds_gm = torch.where(live, ds_g.reshape(-1), torch.zeros_like(ds_o))
+                rel = (ds_o - ds_gm).abs() / ds_o.abs().clamp_min(1e-30)
+                top = torch.topk(torch.where(ds_o != 0, rel, torch.zeros_like(rel)), 6).indices
+                row["d_sigma"] = {"gpu_vs_oracle_live": compare(ds_gm, ds_o),
+                                  "differ_frac_live": float((ds_o != ds_gm)[live].double().mean()),
+                                  "top": [(int(i), int(i) % a.samples, float(ds_o[i]),
+                                           float(ds_gm[i]), float(pos_out[i, 0]))
+                                          for i in top.tolist()]}
+                dc_o = captured["dir_out"].grad.double()[:, :dc_g.shape[-1]]
+                row["d_color"] = {"gpu_vs_oracle": compare(dc_g.reshape(dc_o.shape), dc_o)}
+                rd = (de_o - de_g).abs().amax(1)
+                top = torch.topk(rd, 4).indices.tolist()
+                row["d_enc_top_rows"] = [{"row": r_, "sample": r_ % a.samples,
+                                          "f64": de_o[r_].tolist(), "gpu": de_g[r_].tolist()}
+                                         for r_ in top]
+                # the oracle's f64 hash backward fed with the GPU's dL/denc, quantised as
+                # tcnn's f16 gradient: isolates the GPU hash backward's accumulation
+                x = p._last_hash_bwd[0].double().cpu().numpy()
+                n_ent = int(g64.numel()) // 2
+                cfg_g = (3, 16, 16, 1.3819, int(cfg["instant_ngp"]["encoding"]["log2_hashmap_size"]))
+                gx = torch.from_numpy(ref_tcnn.hashgrid_bwd(x, (de_g * 128).numpy(), cfg_g, n_ent))
+                gx = (gx.half() / 128).double()
+                row["table_from_gpu_denc"] = {"vs_gpu": compare(g_gpu, gx), "vs_f64": compare(gx, g64)}
             rows.append(row)
             print(json.dumps(row), flush=True)
             os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

@@ -230,15 +230,23 @@ class ShardedAdam(torch.optim.Optimizer):
 
     Bytes per step: reduce-scatter 4n + all-gather 2n (f16) against the all-reduce's 8n
     (a ring all-reduce is a reduce-scatter plus an all-gather of f32), and the AdamW pass
-    over n / W elements. Parameters become views into one flat f32 buffer (padded to a
+    over n / W elements. ``exchange="f16"`` (r05) sends the gradient slices as f16 through
+    one all-to-all and sums the W received slices in f32 on the owner -- 2n + 2n bytes,
+    exact when every gradient value is an f16 number, as under the reference numerics
+    (tinycudann's f16 parameter gradients, quantised per rank before the exchange); a
+    gradient that is not f16-exact is refused (``check_f16``, on the first step). Parameters become views into one flat f32 buffer (padded to a
     multiple of W). ``update(segments, step, betas, eps, decoupled)`` applies the update
     (default: the HIP multi-tensor kernel; tests inject a reference)."""
 
     def __init__(self, bucket: FlatGradBucket, param_groups: list, betas=(0.9, 0.999),
                  eps: float = 1e-8, decoupled: bool = True, gather: str = "f16", group=None,
-                 update=hip_adam_update, lr: float = 1e-3, weight_decay: float | None = None):
+                 update=hip_adam_update, lr: float = 1e-3, weight_decay: float | None = None,
+                 exchange: str = "f32", check_f16: bool = True):
         if gather not in ("f16", "f32"):
             raise ValueError("gather: 'f16' or 'f32'")
+        if exchange not in ("f16", "f32"):
+            raise ValueError("exchange: 'f16' or 'f32'")
+        self.exchange, self.check_f16 = exchange, check_f16
         if weight_decay is None:  # FusedAdam's default: torch.optim.AdamW's 1e-2, Adam's 0
             weight_decay = 1e-2 if decoupled else 0.0
         super().__init__(param_groups, dict(lr=lr, betas=tuple(betas), eps=eps,
@@ -302,7 +310,20 @@ class ShardedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lo = self.rank * self.S
-        if self.world > 1:
+        if self.world > 1 and self.exchange == "f16":
+            half = self.bucket.flat.to(torch.float16)
+            # checked on the first step (a guard against pairing it with f32 gradients)
+            if self.check_f16 and self.steps == 0 and not torch.equal(half.float(),
+                                                                      self.bucket.flat):
+                raise ValueError("ShardedAdam(exchange='f16'): the gradient holds values that "
+                                 "are not f16 numbers (quantise them first, or exchange in f32)")
+            recv = torch.empty_like(half)
+            # slice r of every rank's gradient lands on rank r: recv[j * S:(j + 1) * S] is
+            # rank j's contribution, summed here in f32 in rank order
+            dist.all_to_all_single(recv, half, group=self.group)
+            torch.sum(recv.view(self.world, self.S).float(), 0, out=self.grad_shard)
+            self.grad_shard.div_(self.world)
+        elif self.world > 1:
             dist.reduce_scatter_tensor(self.grad_shard, self.bucket.flat, op=dist.ReduceOp.AVG,
                                        group=self.group)
         else:

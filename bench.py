@@ -502,6 +502,7 @@ class IngpJob:
         opt_cfg = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
         opt = pipe.get_optimizer(opt_cfg)
         self.sharded = shard != "off"
+        self.grad_exchange = None
         self.shard = shard
         # the AdamW update joins the graph only without collectives after backward
         self.opt_in_graph = graph and not self.sharded and world == 1
@@ -513,8 +514,14 @@ class IngpJob:
         if world > 1:
             bucket.broadcast_params(0)  # replicas start from rank 0's weights
         if self.sharded:
+            # reference numerics: every rank's gradients are tinycudann's f16 values, so the
+            # reduce-scatter can move f16 (all-to-all + f32 sums on the owner: half the bytes)
+            exch = args.grad_exchange
+            if exch == "auto":
+                exch = "f16" if numerics == "reference" and world > 1 else "f32"
+            self.grad_exchange = exch
             opt = ShardedAdam(bucket, opt.param_groups, betas=opt_cfg["betas"],
-                              eps=opt_cfg["eps"], gather=shard)
+                              eps=opt_cfg["eps"], gather=shard, exchange=exch)
         elif not args.no_fused_zero:
             bucket.fuse_zero_into(opt)  # the AdamW pass zeroes the bucket (no per-step fill)
         if not self.sharded and world == 1:
@@ -696,6 +703,10 @@ def main():
                          "gradient, AdamW on 1/N of the parameters, all-gather of the f16 "
                          "compute copy (f16) or of the f32 parameters (f32), instead of "
                          "all-reduce + replicated AdamW; auto = f16 on more than one rank")
+    ap.add_argument("--grad-exchange", choices=["auto", "f32", "f16"], default="auto",
+                    help="sharded optimizer: gradient slices exchanged as f32 (reduce-scatter) "
+                         "or f16 (all-to-all, f32 sums; exact for the reference numerics' f16 "
+                         "gradients); auto = f16 under reference numerics on more than one rank")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the whole train step as one captured hipGraph "
                          "(atmonr_amd.graph); auto = on for per-rank batches <= 2048 rays, "
@@ -1078,7 +1089,8 @@ def main():
                 "issued_during_backward": bucket.early_issued if bucket.overlap else 0,
                 "backend": dist.get_backend() if world > 1 else None},
             "sharded_optimizer": None if not sharded else {
-                "reduce_scatter_bytes": 4 * bucket.numel,
+                "grad_exchange": job.grad_exchange,
+                "reduce_scatter_bytes": (2 if job.grad_exchange == "f16" else 4) * bucket.numel,
                 "all_gather_bytes": (2 if shard == "f16" else 4) * bucket.numel,
                 "state_floats_per_rank": opt.state_numel(), "gather": shard,
                 "backend": dist.get_backend() if world > 1 else None},

@@ -414,3 +414,66 @@ def test_sharded_adam_scheduler_and_checkpoint():
         assert lrs == [1e-2 * 0.5 ** 5, 3e-3 * 0.5 ** 5]
         for a, c in zip(pa, pc):
             assert torch.equal(a, c)
+
+
+def _f16_exchange_worker(rank, world, port, out):
+    import sys
+
+    from tests.conftest import PKG
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from atmonr_amd.parallel import FlatGradBucket, ShardedAdam
+
+    sizes = [37, 5, 1000, 3, 129]
+    res = {}
+    for exchange in ("f32", "f16"):
+        g0 = torch.Generator().manual_seed(1)
+        ps = [torch.nn.Parameter(torch.randn(n, generator=g0) * 0.1) for n in sizes]
+        b = FlatGradBucket(ps, device=torch.device("cpu"), pad_to=world)
+        opt = ShardedAdam(b, [{"params": ps[:2], "weight_decay": 0.0, "lr": 1e-2},
+                              {"params": ps[2:], "weight_decay": 1e-2, "lr": 3e-3}],
+                          betas=(0.9, 0.99), eps=1e-15, gather="f32",
+                          update=_reference_adamw, exchange=exchange)
+        for step in range(4):
+            b.zero()
+            gg = torch.Generator().manual_seed(1000 * step + rank)
+            with torch.no_grad():
+                for p in ps:  # tinycudann-style per-rank gradients: f16 numbers, many tiny
+                    v = torch.randn(p.shape, generator=gg) * torch.exp(
+                        torch.randn(p.shape, generator=gg) * 4) * 1e-4
+                    p.grad.copy_(v.half().float())
+            opt.step()
+        res[exchange] = [p.detach().clone() for p in ps]
+        if exchange == "f16":  # a gradient that is not an f16 number is refused
+            with torch.no_grad():
+                ps[0].grad.fill_(0.1)
+            opt.steps = 0  # the check runs on the first step
+            try:
+                opt.step()
+                res["refused"] = False
+            except ValueError:
+                res["refused"] = True
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_adam_f16_exchange(world):
+    """ShardedAdam(exchange="f16"): the gradient slices go through one f16 all-to-all and
+    are summed in f32 on their owner (half the bytes of the f32 reduce-scatter). With
+    f16-valued gradients (the reference numerics' tinycudann gradients) the parameters
+    after 4 steps equal the f32 reduce-scatter path's to f32 summation order, at world
+    sizes 2 and 8 (gloo); non-f16 gradients are refused."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_f16_exchange_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        res = out[r]
+        assert res["refused"]
+        for a, b in zip(res["f32"], res["f16"]):
+            assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (r, (a - b).abs().max())
+        for a, b in zip(out[0]["f16"], res["f16"]):
+            assert torch.equal(a, b)  # every replica identical

@@ -1218,3 +1218,73 @@ def test_ingp_field_enc_quad_planes_equal_rows(dev, mma, ref, n_per_ray, R, extr
         _lib.call("anr_ingp_field_fwd", pb, db, code, packed.data_ptr(), planes.data_ptr(),
                   -(8 * M - 8), dirs.data_ptr(), n_per_ray, M, sigma.data_ptr(),
                   color.data_ptr(), nb, s)
+
+
+@pytest.mark.parametrize("ref", [False, True])
+def test_ingp_field_bwd_zero_gradient_tiles(dev, ref):
+    """Tiles whose incoming gradients are zero in every row are skipped by the field
+    backward (r05). Rays with all-zero dL/dcolor and dL/dsigma (two 32-row tiles each,
+    n_per_ray = 64) come back with dL/denc exactly 0, and the other rays' dL/denc equal a
+    launch over those rays alone bit for bit (parameter gradients up to the atomic flush
+    order; build numerics: within their per-wavefront gradient scale): skipping adds or
+    drops nothing. Also a half-zero tile (walked). Build numerics (f16) and reference
+    numerics (anr_ingp_field_bwd_ref16)."""
+    from atmonr_amd import _lib
+
+    width, nhd, nb, n_per_ray, R = 64, 2, 4, 64, 40
+    M = R * n_per_ray
+    g = torch.Generator(device=dev).manual_seed(8)
+    lib = _lib.load()
+    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
+    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
+    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
+    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
+    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
+    dirs = torch.rand(R, 3, device=dev, generator=g)
+    s = _lib.stream(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", pb, db, _lib.F16, pp.data_ptr(), pd.data_ptr(),
+              packed.data_ptr(), s)
+    dcol = (torch.randn(M, nb, device=dev, generator=g) * 1e-2).half().float()
+    dsig = (torch.randn(M, device=dev, generator=g) * 1e-3).half().float()
+    zero_rays = [1, 2, 5, 11, 12, 13, 30, 39]
+    zero = torch.zeros(M, dtype=torch.bool, device=dev)
+    for r in zero_rays:
+        zero[r * n_per_ray:(r + 1) * n_per_ray] = True
+    dcol[zero], dsig[zero] = 0.0, 0.0
+    dcol[20 * n_per_ray:20 * n_per_ray + 16] = 0.0   # half of a tile zero: walked
+    dsig[20 * n_per_ray:20 * n_per_ray + 16] = 0.0
+
+    def run(rays):
+        rows = (torch.tensor(rays, device=dev)[:, None] * n_per_ray +
+                torch.arange(n_per_ray, device=dev)[None]).reshape(-1)
+        m = rows.numel()
+        e_, dc, ds = enc[rows].contiguous(), dcol[rows].contiguous(), dsig[rows].contiguous()
+        dr = dirs[torch.tensor(rays, device=dev)].contiguous()
+        d_enc = torch.full((m, 32), float("nan"), device=dev)
+        g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
+        if ref:
+            _lib.call("anr_ingp_field_bwd_ref16", pb, db, packed.data_ptr(), e_.data_ptr(), 32,
+                      dr.data_ptr(), n_per_ray, m, ds.data_ptr(), dc.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), 128.0, s)
+        else:
+            ws_bytes = lib.anr_ingp_field_bwd_workspace_bytes(pb, db, _lib.F16, m)
+            ws = torch.empty(max(1, ws_bytes // 4), device=dev)
+            _lib.call("anr_ingp_field_bwd", pb, db, _lib.F16, packed.data_ptr(), e_.data_ptr(),
+                      32, dr.data_ptr(), n_per_ray, m, ds.data_ptr(), dc.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), ws.data_ptr(),
+                      ws_bytes, s)
+        return d_enc, g_pos, g_dir
+
+    d_all, gp_all, gd_all = run(list(range(R)))
+    live = [r for r in range(R) if r not in zero_rays]
+    d_live, gp_live, gd_live = run(live)
+    assert torch.all(d_all[zero] == 0)
+    if ref:  # fixed gradient scale (128): every row's f16 chain is the same in both launches
+        assert torch.equal(d_all[~zero], d_live.view(-1, 32))
+        tol = 2e-5
+    else:  # the build numerics' gradient scale is per wavefront, and the wavefronts differ
+        assert (d_all[~zero] - d_live).abs().max().item() <= 1e-2 * d_live.abs().max().item()
+        tol = 1e-2
+    for a_, b_ in ((gp_all, gp_live), (gd_all, gd_live)):
+        assert (a_ - b_).abs().max().item() <= tol * b_.abs().max().item()

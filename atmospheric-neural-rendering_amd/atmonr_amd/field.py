@@ -186,14 +186,24 @@ class IngpFieldFn(torch.autograd.Function):
         pdesc, ddesc = ctypes.byref(pipe.pos_mlp.desc), ctypes.byref(pipe.dir_mlp.desc)
         mma = _mma_code(pipe)
         ls = getattr(pipe, "loss_scale", None)
+        tiles = None
         if ls:
-            # reference numerics: tcnn's loss-scaled f16 backward (anr_ingp_field_bwd_ref16)
+            # reference numerics: tcnn's loss-scaled f16 backward, which also marks the
+            # 32-row tiles whose incoming gradients are all zero (skipped there, and by the
+            # hash-grid backward below without loading them; ANR_TILE_SKIP=0: A/B)
             if ctx.rows is not None:
                 raise _lib.ANRError("reference numerics: no occupancy culling")
-            call("anr_ingp_field_bwd_ref16", pdesc, ddesc, ptr(packed), ptr(enc), ctx.enc_ld,
-                 ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color), d_color.stride(0),
-                 ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir), float(ls), s,
-                 tag="field_bwd")
+            if _TILE_SKIP:
+                tiles = torch.empty((M + 31) // 32, device=dev, dtype=torch.uint8)
+                call("anr_ingp_field_bwd_ref16_tiles", pdesc, ddesc, ptr(packed), ptr(enc),
+                     ctx.enc_ld, ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
+                     d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
+                     float(ls), ptr(tiles), s, tag="field_bwd")
+            else:
+                call("anr_ingp_field_bwd_ref16", pdesc, ddesc, ptr(packed), ptr(enc),
+                     ctx.enc_ld, ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
+                     d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
+                     float(ls), s, tag="field_bwd")
         else:
             ws_bytes = _lib.load().anr_ingp_field_bwd_workspace_bytes(pdesc, ddesc, mma, M)
             ws = torch.empty(max(1, -(-ws_bytes // 4)), device=dev, dtype=torch.float32)
@@ -214,8 +224,13 @@ class IngpFieldFn(torch.autograd.Function):
             pipe._last_d_enc = d_enc
             pipe._last_hash_bwd = (coords, d_enc, g_hash)
             pipe._last_field_grads = (d_sigma, d_color)
-        call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
-             _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
+        if tiles is not None:
+            call("anr_hashgrid_bwd_tiles", ctypes.byref(grid.desc), ptr(coords), 3, M,
+                 ptr(d_enc), _lib.F32, d_enc.stride(0), ptr(g_hash), ptr(tiles), s,
+                 tag="hash_bwd")
+        else:
+            call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
+                 _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
         _done(direct_h, p_hash)
         return (None, None, None, None if direct_h else g_hash, None if direct_p else g_pos,
                 None if direct_d else g_dir, None, None, None)
@@ -233,6 +248,7 @@ def _enc_planes(grid) -> bool:
 
 
 _ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"
+_TILE_SKIP = os.environ.get("ANR_TILE_SKIP", "1") != "0"
 
 
 def field_fused(pipe) -> bool:

@@ -275,6 +275,10 @@ struct Args {
   // > 0: reference numerics (tcnn's loss-scaled f16 backward, anr_ingp_field_bwd_ref16):
   // fixed gradient scale, f16 module-boundary gradients; 0: per-wavefront dynamic scale
   float loss_scale;
+  // nullable: per 32-row tile, 1 if the tile's incoming gradients had a nonzero value (the
+  // tile was walked), 0 if it was skipped (dL/denc rows zero) -- the hash-grid backward
+  // then skips those rows without loading them (anr_hashgrid_bwd_tiles)
+  uint8_t* tile_nz;
 };
 
 // ROWS is a compile-time choice: a run-time test on a.rows in the prefetch paths put a
@@ -1080,7 +1084,9 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       for (int mt = 0; mt < MT; ++mt)
         nz = nz || cur[mt].ds != 0.0f || cur[mt].dc[0] != 0.0f || cur[mt].dc[1] != 0.0f ||
              cur[mt].dc[2] != 0.0f || cur[mt].dc[3] != 0.0f;
-      if (!__any(nz)) {
+      const bool walk = __any(nz);
+      if (a.tile_nz && lane == 0) a.tile_nz[tile] = walk ? 1 : 0;
+      if (!walk) {
         const f4 zero4 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -1648,7 +1654,8 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
                      int64_t n_per_ray, int64_t M, const int32_t* rows, const float* d_sigma,
                      const float* d_color, int64_t d_color_stride, float* d_enc,
                      int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
-                     int64_t workspace_bytes, anr_stream_t stream, float loss_scale = 0.0f) {
+                     int64_t workspace_bytes, anr_stream_t stream, float loss_scale = 0.0f,
+                     uint8_t* tile_nz = nullptr) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_bwd: unsupported pos/dir MLP pair");
   ANR_CHECK_ARG(loss_scale == 0.0f || (loss_scale > 0.0f && mma_dtype == ANR_F16 && rows == nullptr),
@@ -1683,6 +1690,7 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   a.g_dir = g_dir;
   a.rows = rows;
   a.loss_scale = loss_scale;
+  a.tile_nz = tile_nz;
   const int rc = dispatch(v, mma_dtype == ANR_BF16, 2, a, static_cast<float*>(workspace),
                           workspace_bytes, reinterpret_cast<hipStream_t>(stream));
   ANR_CHECK_ARG(rc != 2,
@@ -1751,6 +1759,21 @@ extern "C" int anr_ingp_field_bwd_ref16(const anr_mlp_desc* pos, const anr_mlp_d
   return field_bwd(pos, dir, ANR_F16, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
                    d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, nullptr,
                    0, stream, loss_scale);
+}
+
+extern "C" int anr_ingp_field_bwd_ref16_tiles(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                              const void* packed, const void* enc,
+                                              int64_t enc_stride, const float* dirs,
+                                              int64_t n_per_ray, int64_t M, const float* d_sigma,
+                                              const float* d_color, int64_t d_color_stride,
+                                              float* d_enc, int64_t d_enc_stride, float* g_pos,
+                                              float* g_dir, float loss_scale, uint8_t* tile_nz,
+                                              anr_stream_t stream) {
+  ANR_CHECK_ARG(loss_scale > 0.0f, "anr_ingp_field_bwd_ref16_tiles: loss_scale must be > 0");
+  ANR_CHECK_ARG(tile_nz != nullptr, "anr_ingp_field_bwd_ref16_tiles: null tile_nz");
+  return field_bwd(pos, dir, ANR_F16, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
+                   d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, nullptr,
+                   0, stream, loss_scale, tile_nz);
 }
 
 extern "C" int anr_ingp_field_fwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,

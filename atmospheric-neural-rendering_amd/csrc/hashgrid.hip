@@ -796,7 +796,8 @@ template <int D, typename TG, int XS, int DS, bool COUNT = false>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride_rt, int64_t M,
     int64_t K, const TG* __restrict__ dout, int64_t dout_stride_rt, float* __restrict__ dtable,
-    int skip_zero, unsigned long long* __restrict__ count = nullptr) {
+    int skip_zero, unsigned long long* __restrict__ count = nullptr,
+    const uint8_t* __restrict__ tile_nz = nullptr) {
   constexpr int NC = Corners<D>::NC;
   const int64_t x_stride = XS > 0 ? XS : x_stride_rt;
   const int64_t dout_stride = DS > 0 ? DS : dout_stride_rt;
@@ -941,9 +942,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
       have = false;
     }
   };
-  load_batch(m0, xb, gb);
-  for (int64_t mb = m0; mb < m1; mb += BS) {
-    load_batch(mb + BS, xn, gn);
+  auto do_batch = [&](int64_t mb) {
     bool nzb = false;
 #pragma unroll
     for (int j = 0; j < BS; ++j) nzb = nzb || (mb + j < m1 && to_f32<TG>(gb[j]) != 0.0f);
@@ -960,11 +959,48 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     } else if (skip_zero == 1) {
       flush_all();
     }
+  };
+  auto advance = [&]() {
 #pragma unroll
     for (int j = 0; j < BS; ++j) {
       gb[j] = gn[j];
 #pragma unroll
       for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
+    }
+  };
+  if (tile_nz == nullptr) {
+    load_batch(m0, xb, gb);
+    for (int64_t mb = m0; mb < m1; mb += BS) {
+      load_batch(mb + BS, xn, gn);
+      do_batch(mb);
+      advance();
+    }
+  } else {
+    // anr_hashgrid_bwd_tiles: the field backward marked the 32-row tiles whose dL/dy is
+    // zero in every row (it skipped them); their batches are neither loaded nor walked.
+    // A chunk (K <= 256 rows, a multiple of 32, tile-aligned) is <= 32 batches of 8: one
+    // wave-uniform bit mask, walked in order with the next set batch prefetched.
+    const int nbatch = static_cast<int>((m1 - m0 + BS - 1) / BS);
+    const int ntile = static_cast<int>((m1 - m0 + 31) >> 5);
+    const uint8_t* tf = tile_nz + (m0 >> 5);
+    uint32_t bm = 0;
+    for (int t = 0; t < ntile; ++t)
+      if (tf[t]) bm |= 0xFu << (4 * t);
+    if (nbatch < 32) bm &= (1u << nbatch) - 1u;
+    if (bm) {
+      int j = __builtin_ctz(bm);
+      bm &= bm - 1u;
+      load_batch(m0 + static_cast<int64_t>(j) * BS, xb, gb);
+      while (true) {
+        const bool more = bm != 0u;
+        const int jn = more ? __builtin_ctz(bm) : j;  // no further batch: reload j (unused)
+        load_batch(m0 + static_cast<int64_t>(jn) * BS, xn, gn);
+        do_batch(m0 + static_cast<int64_t>(j) * BS);
+        if (!more) break;
+        advance();
+        j = jn;
+        bm &= bm - 1u;
+      }
     }
   }
   flush_all();
@@ -1371,6 +1407,42 @@ extern "C" int anr_hashgrid_fwd_planes(const anr_hashgrid_desc* d, const float* 
   }
 #undef ANR_HG_PL
   ANR_CHECK_LAUNCH("anr_hashgrid_fwd_planes");
+  return ANR_OK;
+}
+
+extern "C" int anr_hashgrid_bwd_tiles(const anr_hashgrid_desc* d, const float* x,
+                                      int64_t x_stride, int64_t M, const void* dout,
+                                      int32_t dout_dtype, int64_t dout_stride, float* dtable,
+                                      const uint8_t* tile_nz, anr_stream_t stream) {
+  using namespace anr;
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(d && x && dout && dtable && tile_nz, "anr_hashgrid_bwd_tiles: null argument");
+  ANR_CHECK_ARG(M > 0 && x_stride >= d->n_dims &&
+                    dout_stride >= (int64_t)d->n_levels * d->n_features,
+                "anr_hashgrid_bwd_tiles: bad shape/stride");
+  ANR_CHECK_ARG(dout_dtype == ANR_F16 || dout_dtype == ANR_F32, "anr_hashgrid_bwd_tiles: bad dtype");
+  GridLevels G;
+  ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_bwd_tiles: descriptor not initialised");
+  const uint64_t grad_bytes =
+      (static_cast<uint64_t>(G.offset[d->n_levels - 1]) + G.size[d->n_levels - 1]) * 2u * 4u;
+  const int64_t K = pick_chunk_v2(M);
+  if (!(d->n_dims == 3 && d->n_features == 2 && d->n_levels <= 16 && bwd_v2() &&
+        grad_bytes < 0x80000000ull && K % 32 == 0 && x_stride == 3 && dout_stride == 32)) {
+    // outside the tiled walker's shapes: the flags are an optimisation only
+    return anr_hashgrid_bwd(d, x, x_stride, M, dout, dout_dtype, dout_stride, dtable, stream);
+  }
+  const dim3 grid(static_cast<unsigned>(ceil_div(ceil_div(M, K), 4))), block(256);
+  if (dout_dtype == ANR_F16)
+    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, __half, 3, 32>), grid, block, 0,
+                       as_stream(stream), G, d->n_levels, x, x_stride, M, K,
+                       static_cast<const __half*>(dout), dout_stride, dtable, bwd_skip_zero(),
+                       nullptr, tile_nz);
+  else
+    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, float, 3, 32>), grid, block, 0,
+                       as_stream(stream), G, d->n_levels, x, x_stride, M, K,
+                       static_cast<const float*>(dout), dout_stride, dtable, bwd_skip_zero(),
+                       nullptr, tile_nz);
+  ANR_CHECK_LAUNCH("anr_hashgrid_bwd_tiles");
   return ANR_OK;
 }
 

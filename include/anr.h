@@ -179,6 +179,16 @@ int anr_hashgrid_bwd_count_requests(const anr_hashgrid_desc* d, const float* x,
 /* Backward: dout (M, L*F) (dout_dtype, row stride dout_stride) -> dtable (n_params)
  * f32, ACCUMULATED (caller zeroes). Duplicate corner updates inside a wavefront are
  * pre-summed before the f32 atomics (samples along one ray share cells). */
+/* anr_hashgrid_bwd with the field backward's per-tile flags (r05): tile_nz[t] = 0 marks
+ * rows [32 t, 32 t + 32) whose dL/dy is zero in every row (anr_ingp_field_bwd_ref16_tiles
+ * writes them); the v2 walker neither loads nor walks those rows (their contributions
+ * are zero). Same result as anr_hashgrid_bwd for such inputs; shapes outside the tiled
+ * walker (not 3-D / 2 features / <= 16 levels, strides other than (3, 32), chunks not a
+ * multiple of 32 rows) run anr_hashgrid_bwd and ignore the flags. */
+int anr_hashgrid_bwd_tiles(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
+                           int64_t M, const void* dout, int32_t dout_dtype, int64_t dout_stride,
+                           float* dtable, const uint8_t* tile_nz, anr_stream_t stream);
+
 /* Level-quad-plane forward (r05; hashgrid.hip forward v9, one lane per sample): the same
  * features as anr_hashgrid_fwd with f16 output, laid out as planes of four levels: level
  * l, feature f of row m at out[(l / 4) * plane_stride + 8 m + 2 (l % 4) + f]
@@ -517,6 +527,17 @@ int anr_ingp_field_bwd_ref16(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
                              int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
                              float* g_pos, float* g_dir, float loss_scale,
                              anr_stream_t stream);
+/* anr_ingp_field_bwd_ref16 that also writes, per 32-row tile t of the M rows, tile_nz[t]
+ * = 1 if any row of the tile had a nonzero dL/dcolor or dL/dsigma (the tile was walked)
+ * and 0 otherwise (skipped: its dL/denc rows are written as 0). tile_nz: ceil(M / 32)
+ * bytes of device memory, for anr_hashgrid_bwd_tiles. */
+int anr_ingp_field_bwd_ref16_tiles(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                   const void* packed, const void* enc, int64_t enc_stride,
+                                   const float* dirs, int64_t n_per_ray, int64_t M,
+                                   const float* d_sigma, const float* d_color,
+                                   int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
+                                   float* g_pos, float* g_dir, float loss_scale,
+                                   uint8_t* tile_nz, anr_stream_t stream);
 /* anr_mlp_bwd_ws in f16 with tcnn's fixed loss scale: dL/dinput written as
  * f16(f16(g_scaled)/loss_scale). Specialised (fused) MLP shapes only. */
 int anr_mlp_bwd_ref16(const anr_mlp_desc* d, const void* params, const void* in,

@@ -1288,3 +1288,35 @@ def test_ingp_field_bwd_zero_gradient_tiles(dev, ref):
         tol = 1e-2
     for a_, b_ in ((gp_all, gp_live), (gd_all, gd_live)):
         assert (a_ - b_).abs().max().item() <= tol * b_.abs().max().item()
+
+
+@pytest.mark.parametrize("M", [262144, 1048576, 300000])
+def test_hashgrid_bwd_tiles_equals_plain(dev, M):
+    """anr_hashgrid_bwd_tiles skips the 32-row tiles flagged zero (the reference-numerics
+    field backward's all-zero tiles) without loading them: with dL/dy zero on exactly those
+    rows (plus tiles flagged 1 that are zero anyway, and a ragged end) the table gradient
+    equals anr_hashgrid_bwd's up to the f32 atomic order. M = 300,000 has chunks that are
+    not a multiple of 32 rows: the flags are ignored there (plain walker)."""
+    from atmonr_amd import _lib
+
+    cfg = (3, 16, 16, 1.3819, 19)
+    d = _lib.hashgrid_desc(*cfg[:1], cfg[1], 2, cfg[2], cfg[3], cfg[4])
+    x = _grid_inputs(dev, cfg, M, True).to(dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    dout = torch.randn(M, 32, device=dev, generator=g) * 1e-3
+    nt = -(-M // 32)
+    flags = (torch.rand(nt, device=dev, generator=g) < 0.4).to(torch.uint8)
+    rows_zero = flags.repeat_interleave(32)[:M] == 0
+    dout[rows_zero] = 0.0
+    flags[:: 7] = 1  # flagged walkable but zero where it was zeroed: still exact
+    s = _lib.stream(dev)
+    ga = torch.zeros(d.n_params, device=dev)
+    gb = torch.zeros(d.n_params, device=dev)
+    _lib.call("anr_hashgrid_bwd", ctypes.byref(d), x.data_ptr(), 3, M, dout.data_ptr(), _lib.F32,
+              32, ga.data_ptr(), s)
+    _lib.call("anr_hashgrid_bwd_tiles", ctypes.byref(d), x.data_ptr(), 3, M, dout.data_ptr(),
+              _lib.F32, 32, gb.data_ptr(), flags.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.isfinite(gb).all()
+    assert (ga - gb).abs().max().item() <= 1e-5 * ga.abs().max().item()
+    assert ((ga != 0) == (gb != 0)).float().mean().item() > 0.9999

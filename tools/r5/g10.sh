@@ -23,5 +23,10 @@ for k, v in d.items():
     if k.startswith("psnr_reference_semantics") and isinstance(v, list) and v and "iteration" in v[0]:
         print(k, [(r["iteration"], round(r["delta_reference_numerics_db"], 4)) for r in v])
 PY
-timeout -k 10 400 python -u bench.py --no-cpu-baseline > $O/bench.json.log 2>&1 || { tail -30 $O/bench.json.log; exit 1; }
-python3 tools/r5/bench_line.py $O/bench.json.log r5
+timeout -k 10 300 python -u tools/r5/hash_bwd_state.py dump --steps 160 --out /tmp/hb_ref160.pt > $O/state160.log 2>&1 || { tail -20 $O/state160.log; exit 1; }
+grep state $O/state160.log
+rm -f /tmp/hb_ref160.pt
+for ts in 1 0; do
+ANR_TILE_SKIP=$ts timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-alt-numerics > $O/bench_ts$ts.json.log 2>&1 || { tail -30 $O/bench_ts$ts.json.log; exit 1; }
+python3 tools/r5/bench_line.py $O/bench_ts$ts.json.log tileskip$ts
+done

@@ -56,6 +56,14 @@ def dump(a):
     b8 = rows[: (M // 8) * 8].view(-1, 8)
     live = b8.any(1)
     st["rows_nonzero_in_live_batches8"] = b8[live].float().mean().item()
+    # field-backward tiles (32 samples) whose incoming gradients are all zero
+    ds_, dc_ = pipe._last_field_grads
+    zc = (dc_.reshape(M, -1) == 0).all(1)
+    zs = (ds_.reshape(M) == 0)
+    for T in (16, 32):
+        n = M // T
+        st[f"tiles{T}_color_grad_zero"] = zc[: n * T].view(n, T).all(1).float().mean().item()
+        st[f"tiles{T}_all_grad_zero"] = (zc & zs)[: n * T].view(n, T).all(1).float().mean().item()
     print("state", a.numerics, "steps", a.steps, st, flush=True)
     torch.save({"coords": coords.contiguous(), "d_enc": d_enc.contiguous(), "stats": st,
                 "numerics": a.numerics}, a.out)

@@ -188,9 +188,10 @@ class IngpFieldFn(torch.autograd.Function):
         ls = getattr(pipe, "loss_scale", None)
         tiles = None
         if ls:
-            # reference numerics: tcnn's loss-scaled f16 backward, which also marks the
-            # 32-row tiles whose incoming gradients are all zero (skipped there, and by the
-            # hash-grid backward below without loading them; ANR_TILE_SKIP=0: A/B)
+            # reference numerics: tcnn's loss-scaled f16 backward. ANR_TILE_SKIP=1: it also
+            # marks the 32-row tiles whose incoming gradients are all zero and the hash-grid
+            # backward skips them without loading. Off by default: measured no faster than
+            # the per-sample skip alone (2.782 vs 2.769 ms/step, profiles/r05_tile_skip_ab.log)
             if ctx.rows is not None:
                 raise _lib.ANRError("reference numerics: no occupancy culling")
             if _TILE_SKIP:
@@ -248,7 +249,7 @@ def _enc_planes(grid) -> bool:
 
 
 _ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"
-_TILE_SKIP = os.environ.get("ANR_TILE_SKIP", "1") != "0"
+_TILE_SKIP = os.environ.get("ANR_TILE_SKIP", "0") != "0"
 
 
 def field_fused(pipe) -> bool:

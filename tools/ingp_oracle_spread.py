@@ -31,6 +31,11 @@ from oracle import ref_ingp  # noqa: E402
 from tests import ingp_psnr  # noqa: E402
 
 
+def _progress(out):
+    it = next(iter(out.values()))[-1]["iteration"]
+    print("checkpoint", it, {k: round(v[-1]["psnr"], 4) for k, v in out.items()}, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--runs", type=int, default=3)
@@ -44,6 +49,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--semantics", default="reference")
+    ap.add_argument("--scene-device", default="cpu",
+                    help="cuda: build the scene on the GPU exactly as the PSNR test does "
+                    "(device libm), so the unperturbed run reproduces the test's oracle")
     ap.add_argument("--ref-acc", default="cuda", help="cuda | cpu (oracle/ref_ingp.py)")
     ap.add_argument("--perturb", default="grad", help="grad: one f16 ulp of one ray's "
                     "loss gradient at step 0; dirs: every ray direction by one f32 ulp; "
@@ -58,9 +66,12 @@ def main():
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
     from atmonr_amd.pipelines.instant_ngp import InstantNGPPipeline
 
-    scene = SyntheticHARP2Dataset(n_views=8, img_size=16, device=torch.device("cpu"), seed=0)
+    scene = SyntheticHARP2Dataset(n_views=8, img_size=16, device=torch.device(a.scene_device),
+                                  seed=0)
     cfg = ge._ingp_config(a.samples)
     p = InstantNGPPipeline(cfg, scene, dtype=torch.float16, fused=True, seed=5)
+    if a.scene_device != "cpu":
+        p.send_tensors_to(torch.device(a.scene_device))
     state = p.state_dict()
     pp = scene.get_point_preprocessor("horizontal")
     opt = {"lr": 1e-2, "betas": [0.9, 0.99], "eps": 1e-15, "weight_decay": 1e-2}
@@ -98,7 +109,7 @@ def main():
     t0 = time.time()
     cps = tuple(int(c) for c in a.checkpoints.split(",") if int(c) <= a.iters)
     res = ingp_psnr.train_side_by_side(runners, scene, a.samples, checkpoints=cps,
-                                       batch=a.batch)
+                                       batch=a.batch, progress=_progress)
     for name, out in res.items():
         print(name, [round(r["psnr"], 4) for r in out], flush=True)
     print(f"{time.time() - t0:.0f}s")

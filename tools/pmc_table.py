@@ -2,8 +2,8 @@
 
     python tools/pmc_table.py gpurun_out/sq_bench [kernel-substring ...]
 
-Each counter: median over the second half of the kernel's launches (the bench network
-is alive from step ~7; tools/liveness.py)."""
+Each counter: median over the second half of the kernel's launches (bench.py settles the
+reference numerics for 150 steps first, so that half is the settled state)."""
 
 from __future__ import annotations
 
@@ -13,14 +13,13 @@ import glob
 import os
 import sys
 
-KERNELS = {"hash_fwd": "hashgrid_fwd_v6_kernel<3, __half, __half>",
-           "hash_fwd_v1": "hashgrid_fwd_kernel<3, 2, __half, __half>",
-           "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32, false>",
-           "field_fwd": "field::fwd_kernel<64, 2, false, false, true>",
-           "field_bwd": "field::bwd_rt_kernel<64, 2, true, false, false>",
+KERNELS = {"hash_fwd": "hashgrid_fwd_planes_kernel<",
+           "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32",
+           "field_fwd": "field::fwd_kernel<64, 2",
+           "field_bwd": "field::bwd_rt_kernel<64, 2, true, false",
            "sampler": "sample_uniform_bins_kernel",
-           "comp_fwd": "rb::fwd_kernel<float, 4, 1, 4>",
-           "comp_bwd": "rb::bwd_kernel<float, 4, 1, 4>"}
+           "comp_fwd": "ref16::fwd_kernel<",
+           "comp_bwd": "ref16::bwd_kernel<"}
 
 
 def main(src):

@@ -304,11 +304,36 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
     flops = 3.0 * (nerf_mlp_flops(pipe.nerf["coarse"], batch_size * nc)
                    + nerf_mlp_flops(pipe.nerf["fine"], batch_size * (nc + nf)))
     tfs = flops / (ms * 1e-3) / 1e12
-    roofline = {"kernel": "nerf_mlp_gemms (library f32 GEMMs, whole-step time)",
+    from atmonr_amd import nerf_model
+
+    native = nerf_model._NATIVE
+    roofline = {"kernel": ("nerf_linear_{fwd,dx,dw} (csrc/nerf_mlp.hip f32 MFMA GEMMs), "
+                           "whole-step time" if native else
+                           "nerf_mlp_gemms (library f32 GEMMs, whole-step time)"),
                 "bound": "mfma", "achieved": round(tfs, 2), "peak": peaks["mfma_f32_tfs"],
                 "unit": "TFLOP/s", "frac": round(tfs / peaks["mfma_f32_tfs"], 4), "traffic": None,
                 "algorithmic_flops": flops, "units_per_launch": batch_size,
                 "flops_per_unit": flops / batch_size}
+    kernels = None
+    if native and not args.no_kernel_timer:
+        # untimed profiling pass: HIP events around every dense-layer launch (same stream)
+        tags = {"nerf_linear_fwd", "nerf_linear_dx", "nerf_linear_dw"}
+        prof_steps = 3
+        with _lib.KernelTimer(only=tags) as kt:
+            for _ in range(prof_steps):
+                step()
+        summ = kt.summary()
+        kernels = {k: {"ms_per_step": round(v["total_ms"] / prof_steps, 3),
+                       "launches_per_step": v["launches"] // prof_steps}
+                   for k, v in sorted(summ.items())}
+        gemm_ms = sum(v["total_ms"] for v in summ.values()) / prof_steps
+        if gemm_ms > 0:
+            gtfs = flops / (gemm_ms * 1e-3) / 1e12
+            roofline["gemm_kernels"] = {
+                "ms_per_step": round(gemm_ms, 3), "achieved": round(gtfs, 2),
+                "frac": round(gtfs / peaks["mfma_f32_tfs"], 4),
+                "source": "HIP events around each nerf_linear_* launch, untimed pass of "
+                          f"{prof_steps} steps; flops = the step's algorithmic MLP flops"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline
@@ -328,6 +353,7 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
                                    "samples/ray), full train step (fwd+loss+bwd+Adam)",
                        "global_batch": batch_size * world, "parallelism": f"dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "peaks": peaks,
+            "kernels": kernels, "mlp": "native" if native else "library",
             "final_loss": round(final_loss, 6),
             "scene_build_s": round(t_scene, 2)}), flush=True)
     if world > 1:

@@ -407,6 +407,38 @@ int anr_posenc_bwd(const anr_posenc_desc* d, const float* x, int64_t P, const fl
  * NULL then). */
 int anr_relu_bwd_colsum(const float* g, const float* y, int64_t M, int32_t C, float* g_out,
                         float* partial, int32_t n_parts, anr_stream_t stream);
+/* AtmoNeRF dense layers on the f32 matrix cores (csrc/nerf_mlp.hip). They replace the
+ * nn.Linear / torch.cat / F.relu calls of src/atmonr/models/nerf.py:48-93 and their
+ * autograd backward. Operands are row-major f32 with 16-byte-aligned rows: every leading
+ * dimension and segment width is a multiple of 4.
+ *
+ * Forward: y (M x n, row stride ldy) = [a1 | a2] W^T + bias, then ReLU if relu != 0.
+ *   a1 is M x q1 and a2 is M x q2 (q2 = 0: none); they are the fc6 skip and fc10
+ *   direction concats, read in place. W is n x (q1+q2), as nn.Linear.weight. bias is
+ *   nullable. */
+int anr_nerf_linear_fwd(const float* a1, int64_t lda1, int32_t q1, const float* a2,
+                        int64_t lda2, int32_t q2, int64_t M, const float* w, int32_t n,
+                        const float* bias, int32_t relu, float* y, int64_t ldy,
+                        anr_stream_t stream);
+/* Input gradient: [dx1 | dx2] (M x (p1+p2)) = g (M x n) W, with wt = W^T
+ * ((p1+p2) x n, row stride ldwt).
+ *   If n % 4 != 0, g's and wt's columns n .. round_up(n, 4) must exist and be zero.
+ *   dx1 (first p1 columns) is zeroed where mask (M x p1, nullable) is <= 0. That is the
+ *   ReLU backward of the layer whose output the input was.
+ *   dx2 (last p2 columns) is written, or added to if acc2 != 0. */
+int anr_nerf_linear_dx(const float* g, int64_t ldg, int64_t M, int32_t n, const float* wt,
+                       int64_t ldwt, int32_t p1, int32_t p2, const float* mask, int64_t ldm,
+                       float* dx1, int64_t ldx1, float* dx2, int64_t ldx2, int32_t acc2,
+                       anr_stream_t stream);
+/* Parameter gradients, ACCUMULATED: dw (n x (q1+q2), contiguous) += g^T [a1 | a2], and
+ * db (n, nullable) += the column sums of g.
+ *   g's columns n .. round_up(n, 4) must be zero.
+ *   M is split over blocks into f32 partials in ws (anr_nerf_linear_dw_workspace bytes,
+ *   16-byte aligned), summed in a fixed order: the result is deterministic. */
+int64_t anr_nerf_linear_dw_workspace(int64_t M, int32_t n, int32_t k);
+int anr_nerf_linear_dw(const float* g, int64_t ldg, int64_t M, int32_t n, const float* a1,
+                       int64_t lda1, int32_t q1, const float* a2, int64_t lda2, int32_t q2,
+                       float* dw, float* db, void* ws, int64_t ws_bytes, anr_stream_t stream);
 /* sample_pdf forward, one wavefront per ray (3 <= Nc <= 64, 1 <= Nf <= 256).
  *   weights: coarse render weights, element (b, j) at b*w_ray_stride + j*w_sample_stride
  *   (channel 0 of (B, Nc, S)); z_coarse (B,Nc) f32 ascending; u (B,Nf) f32 draws.

@@ -274,3 +274,143 @@ def test_relu_bwd_colsum_matches_torch(dev, M, C):
     db = partial.sum(0).double()
     want = ref.double().sum(0)
     assert torch.all((db - want).abs() <= 1e-5 * ref.double().abs().sum(0) + 1e-30)
+
+
+# ------------------------------------------------------------------ AtmoNeRF dense layers
+# csrc/nerf_mlp.hip against f64 torch on the same f32 operands: f32 MFMA sums in another
+# order than hipBLASLt's, so the bar is f32 summation error (rel 1e-5 of sum |a·b| terms).
+def _f32_bar(a, b):
+    return 2e-5 * (a.double().abs() @ b.double().abs().t()) + 1e-30
+
+
+@pytest.mark.parametrize("M,q1,q2,n,relu", [(1000, 76, 0, 256, 1), (4096, 256, 76, 256, 1),
+                                            (777, 256, 24, 128, 1), (300, 256, 0, 257, 0),
+                                            (64, 128, 0, 4, 0), (0, 256, 0, 256, 1)])
+def test_nerf_linear_fwd_matches_f64(dev, M, q1, q2, n, relu):
+    from atmonr_amd import _lib
+
+    gen = torch.Generator(device=dev).manual_seed(M + n)
+    lda = q1 + q2 + 4       # strided rows, as the encoding and the padded fc9 output are
+    x = torch.randn(M, lda, device=dev, generator=gen)
+    w = torch.randn(n, q1 + q2, device=dev, generator=gen) * 0.1
+    b = torch.randn(n, device=dev, generator=gen)
+    ld = (n + 3) // 4 * 4
+    y = torch.full((M, ld), float("nan"), device=dev)
+    a2 = x[:, q1:] if q2 else None
+    _lib.call("anr_nerf_linear_fwd", _lib.ptr(x), lda, q1, _lib.ptr(a2), lda, q2, M,
+              _lib.ptr(w), n, _lib.ptr(b), relu, _lib.ptr(y), ld, _lib.stream(dev))
+    a = x[:, : q1 + q2]
+    want = a.double() @ w.double().t() + b.double()
+    bar = _f32_bar(a, w) + 1e-6 * b.double().abs()
+    if relu:
+        want = want.clamp_min(0)
+    assert torch.all((y[:, :n].double() - want).abs() <= bar)
+
+
+@pytest.mark.parametrize("M,n,p1,p2,acc2", [(1000, 256, 256, 76, 0), (1000, 256, 0, 76, 1),
+                                            (555, 257, 256, 0, 0), (300, 4, 128, 0, 0),
+                                            (4096, 128, 0, 256, 0)])
+def test_nerf_linear_dx_matches_f64(dev, M, n, p1, p2, acc2):
+    """dX = G W with the ReLU mask of the saved input on the first p1 columns (exactly
+    torch's threshold_backward) and an accumulating second segment."""
+    from atmonr_amd import _lib
+
+    gen = torch.Generator(device=dev).manual_seed(M + n + p1)
+    nr = (n + 3) // 4 * 4
+    g = torch.zeros(M, nr, device=dev)
+    g[:, :n] = torch.randn(M, n, device=dev, generator=gen)
+    w = torch.randn(n, p1 + p2, device=dev, generator=gen) * 0.1
+    wt = torch.zeros(p1 + p2, nr, device=dev)
+    wt[:, :n] = w.t()
+    mask = torch.relu(torch.randn(M, max(p1, 1), device=dev, generator=gen))
+    dx1 = torch.full((M, max(p1, 1)), float("nan"), device=dev)
+    base = torch.randn(M, p2 + 4, device=dev, generator=gen)
+    dx2 = base.clone()
+    _lib.call("anr_nerf_linear_dx", _lib.ptr(g), nr, M, n, _lib.ptr(wt), nr, p1, p2,
+              _lib.ptr(mask) if p1 else None, mask.stride(0), _lib.ptr(dx1) if p1 else None,
+              dx1.stride(0), _lib.ptr(dx2) if p2 else None, dx2.stride(0), acc2,
+              _lib.stream(dev))
+    full = g[:, :n].double() @ w.double()
+    bar = _f32_bar(g[:, :n], w.t())
+    if p1:
+        want = torch.where(mask[:, :p1] > 0, full[:, :p1], torch.zeros_like(full[:, :p1]))
+        assert torch.all((dx1[:, :p1].double() - want).abs() <= bar[:, :p1])
+        assert torch.equal(dx1[:, :p1][mask[:, :p1] <= 0], torch.zeros_like(dx1[:, :p1][mask[:, :p1] <= 0]))
+    if p2:
+        want2 = full[:, p1:] + (base[:, :p2].double() if acc2 else 0)
+        assert torch.all((dx2[:, :p2].double() - want2).abs()
+                         <= bar[:, p1:] + 1e-6 * base[:, :p2].double().abs())
+        assert torch.equal(dx2[:, p2:], base[:, p2:])
+
+
+@pytest.mark.parametrize("M,n,q1,q2", [(786432, 256, 256, 0), (1000, 257, 256, 0),
+                                       (4099, 128, 256, 24), (5000, 256, 256, 76),
+                                       (300, 4, 128, 0), (0, 256, 76, 0)])
+def test_nerf_linear_dw_matches_f64(dev, M, n, q1, q2):
+    """dW += G^T [A1 | A2] and db += colsum(G), accumulated, deterministic (two launches
+    give identical bits)."""
+    from atmonr_amd import _lib
+
+    gen = torch.Generator(device=dev).manual_seed(M + n + q2)
+    nr = (n + 3) // 4 * 4
+    g = torch.zeros(M, nr, device=dev)
+    g[:, :n] = torch.randn(M, n, device=dev, generator=gen)
+    lda = q1 + q2 + 8
+    x = torch.randn(M, lda, device=dev, generator=gen)
+    K = q1 + q2
+    dw0 = torch.randn(n, K, device=dev, generator=gen)
+    db0 = torch.randn(n, device=dev, generator=gen)
+    lib = _lib.load()
+    ws = torch.empty(max(16, lib.anr_nerf_linear_dw_workspace(M, n, K)) // 4, device=dev)
+    outs = []
+    for _ in range(2):
+        dw, db = dw0.clone(), db0.clone()
+        _lib.call("anr_nerf_linear_dw", _lib.ptr(g), nr, M, n, _lib.ptr(x), lda, q1,
+                  _lib.ptr(x[:, q1:]) if q2 else None, lda, q2, _lib.ptr(dw), _lib.ptr(db),
+                  _lib.ptr(ws), ws.numel() * 4, _lib.stream(dev))
+        outs.append((dw, db))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    dw, db = outs[0]
+    gd, xd = g[:, :n].double(), x[:, :K].double()
+    want = dw0.double() + gd.t() @ xd
+    bar = 2e-5 * (gd.abs().t() @ xd.abs()) + 1e-6 * dw0.double().abs() + 1e-30
+    assert torch.all((dw.double() - want).abs() <= bar)
+    wantb = db0.double() + gd.sum(0)
+    assert torch.all((db.double() - wantb).abs() <= 2e-5 * gd.abs().sum(0) + 1e-6 * db0.double().abs() + 1e-30)
+
+
+@pytest.mark.parametrize("vol,M", [(1, 4096 * 2 + 7), (4, 3000)])
+def test_atmonerf_native_matches_library_path(dev, vol, M):
+    """AtmoNeRF.forward on csrc/nerf_mlp.hip (_AtmoNeRFFn) against the library-GEMM path
+    (torch.nn.Linear, autograd) on the same parameters, inputs and noise: outputs and every
+    gradient (parameters and dL/dx_pos, the fc1 + fc6 skip sum) within f32 GEMM
+    rounding."""
+    from atmonr_amd import nerf_model
+
+    torch.manual_seed(7)
+    net = nerf_model.AtmoNeRF(76, 24, 4, vol, 256).to(dev)
+    net.train()
+    gen = torch.Generator(device=dev).manual_seed(M)
+    x0 = torch.randn(M, 100, device=dev, generator=gen)
+    noise = torch.randn(M, vol, device=dev, generator=gen)
+    dcol = torch.randn(M, 4, device=dev, generator=gen)
+    dsig = torch.randn(M, vol, device=dev, generator=gen)
+    res = {}
+    for mode in ("native", "torch"):
+        nerf_model._NATIVE = mode == "native"
+        try:
+            net.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            color, sigma = net(x, noise)
+            ((color * dcol).sum() + (sigma * dsig).sum()).backward()
+            res[mode] = (color.detach(), sigma.detach(), x.grad.clone(),
+                         [p.grad.clone() for p in net.params_in_order()])
+        finally:
+            nerf_model._NATIVE = True
+    (cn, sn, xn, gn), (ct, s_t, xt, gt) = res["native"], res["torch"]
+    close(cn, ct, rel=1e-4, atol=1e-6, what="color")
+    close(sn, s_t, rel=1e-4, atol=1e-5, what="sigma")
+    # the direction columns are data: the native path leaves their gradient zero
+    close(xn[:, :76], xt[:, :76], rel=1e-3, atol=1e-6, what="dL/dx_pos")
+    for i, (a, b) in enumerate(zip(gn, gt)):
+        close(a, b, rel=1e-3, atol=1e-6, what=f"param {i}")

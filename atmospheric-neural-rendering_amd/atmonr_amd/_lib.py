@@ -139,10 +139,9 @@ _SIGNATURES = {
     "anr_posenc_bwd": (c_int32, [POINTER(PosencDesc), _P, c_int64, _P, c_int64, _P, _P]),
     "anr_relu_bwd_colsum": (c_int32, [_P, _P, c_int64, c_int32, _P, _P, c_int32, _P]),
     "anr_nerf_linear_fwd": (c_int32, [_P, c_int64, c_int32, _P, c_int64, c_int32, c_int64, _P,
-                                      c_int32, _P, c_int32, _P, c_int64, _P]),
+                                      c_int32, _P, c_int32, _P, c_int64, _P, _P]),
     "anr_nerf_linear_dx": (c_int32, [_P, c_int64, c_int64, c_int32, _P, c_int64, c_int32,
-                                     c_int32, _P, c_int64, _P, c_int64, _P, c_int64, c_int32,
-                                     _P]),
+                                     c_int32, _P, _P, c_int64, _P, c_int64, c_int32, _P]),
     "anr_nerf_linear_dw_workspace": (c_int64, [c_int64, c_int32, c_int32]),
     "anr_nerf_linear_dw": (c_int32, [_P, c_int64, c_int64, c_int32, _P, c_int64, c_int32, _P,
                                      c_int64, c_int32, _P, _P, _P, c_int64, _P]),

@@ -59,8 +59,9 @@ def _wt(layer: nn.Linear) -> tuple[torch.Tensor, int]:
     return t, ld
 
 
-def _mlp_forward(net: "AtmoNeRF", x: torch.Tensor, pos_only: bool):
-    """The layer stack on csrc/nerf_mlp.hip; returns (y1..y8, y9 padded, y10, y11)."""
+def _mlp_forward(net: "AtmoNeRF", x: torch.Tensor, pos_only: bool, masks: list | None = None):
+    """The layer stack on csrc/nerf_mlp.hip; returns (y1..y8, y9 padded, y10, y11). With
+    ``masks`` (a list) the ReLU layers also write their bitmasks there, by layer number."""
     from . import _lib
 
     M, dev = x.shape[0], x.device
@@ -73,9 +74,13 @@ def _mlp_forward(net: "AtmoNeRF", x: torch.Tensor, pos_only: bool):
         n = layer.out_features
         ld = ld or _r4(n)
         y = torch.empty(M, ld, device=dev, dtype=torch.float32)
+        bits = None
+        if masks is not None and relu:
+            bits = torch.empty(M, (n + 63) // 64, device=dev, dtype=torch.int64)
+            masks[i] = bits
         _lib.call("anr_nerf_linear_fwd", _lib.ptr(a1), lda1, q1, _lib.ptr(a2), lda2, q2, M,
-                  _lib.ptr(layer.weight), n, _lib.ptr(layer.bias), relu, _lib.ptr(y), ld, st,
-                  tag="nerf_linear_fwd")
+                  _lib.ptr(layer.weight), n, _lib.ptr(layer.bias), relu, _lib.ptr(y), ld,
+                  _lib.ptr(bits), st, tag="nerf_linear_fwd")
         return y
 
     ys = [lin(1, x, ldx, pc)]
@@ -85,9 +90,7 @@ def _mlp_forward(net: "AtmoNeRF", x: torch.Tensor, pos_only: bool):
     for i in (7, 8):
         ys.append(lin(i, ys[-1], h, h))
     n9 = net.fc9.out_features
-    y9 = lin(9, ys[-1], h, h, relu=0)
-    if n9 < y9.shape[1]:
-        y9[:, n9:].zero_()   # the pad columns stay zero (the backward's G9 needs them)
+    y9 = lin(9, ys[-1], h, h, relu=0)   # its pad columns come out zero
     ys.append(y9)
     if pos_only:
         return ys
@@ -109,7 +112,8 @@ class _AtmoNeRFFn(torch.autograd.Function):
         from . import _lib
 
         _lib.grad_use(*params)
-        ys = _mlp_forward(net, x, pos_only=False)
+        masks = [None] * 12
+        ys = _mlp_forward(net, x, pos_only=False, masks=masks)
         h, n9 = net.hidden_dim, net.fc9.out_features
         sig = ys[8][:, h:n9]
         if noise is not None:
@@ -118,7 +122,8 @@ class _AtmoNeRFFn(torch.autograd.Function):
         out = net.fc11.out_features
         color = torch.sigmoid(ys[10][:, :out])
         ctx.net = net
-        ctx.save_for_backward(x, *ys[:10], color, sigma)
+        ctx.save_for_backward(x, *ys[:10], color, sigma, *[masks[i] for i in range(1, 11)
+                                                           if i != 9])
         return color, sigma
 
     @staticmethod
@@ -126,7 +131,9 @@ class _AtmoNeRFFn(torch.autograd.Function):
         from . import _lib
 
         net = ctx.net
-        x, *ys, color, sigma = ctx.saved_tensors
+        x, *rest = ctx.saved_tensors
+        ys, (color, sigma), mb = rest[:10], rest[10:12], rest[12:]
+        bits = dict(zip([i for i in range(1, 11) if i != 9], mb))   # layer -> ReLU bitmask
         M, dev = x.shape[0], x.device
         h, pc, dc = net.hidden_dim, net.pos_channels, net.dir_channels
         st, ldx = _lib.stream(dev), x.stride(0)
@@ -148,12 +155,13 @@ class _AtmoNeRFFn(torch.autograd.Function):
             _lib.grad_done(*[p for p, d in ((L.weight, w_direct), (L.bias, b_direct)) if d])
 
         def dgrad(i, g, p1, mask=None, dx2=None, p2=0, acc2=0):
+            """dL/d(input of layer i); ``mask`` = the layer whose ReLU output it is."""
             L = layers[i - 1]
             wt, ldwt = _wt(L)
             dx1 = torch.empty(M, max(p1, 1), device=dev, dtype=torch.float32) if p1 else None
             _lib.call("anr_nerf_linear_dx", _lib.ptr(g), g.stride(0), M, L.out_features,
-                      _lib.ptr(wt), ldwt, p1, p2, _lib.ptr(mask),
-                      mask.stride(0) if mask is not None else 0, _lib.ptr(dx1),
+                      _lib.ptr(wt), ldwt, p1, p2,
+                      _lib.ptr(bits[mask]) if mask is not None else None, _lib.ptr(dx1),
                       dx1.stride(0) if dx1 is not None else 0, _lib.ptr(dx2),
                       dx2.stride(0) if dx2 is not None else 0, acc2, st,
                       tag="nerf_linear_dx")
@@ -166,7 +174,7 @@ class _AtmoNeRFFn(torch.autograd.Function):
             g11[:, :out] = dcolor * (1 - color) * color
         y10 = ys[9]
         wgrad(11, g11, y10, y10.stride(0), y10.shape[1])
-        g10 = dgrad(11, g11, layers[9].out_features, mask=y10)
+        g10 = dgrad(11, g11, layers[9].out_features, mask=10)
         y9 = ys[8]
         wgrad(10, g10, y9, y9.stride(0), h, x[:, pc:], ldx, dc)
         n9 = layers[8].out_features
@@ -177,16 +185,16 @@ class _AtmoNeRFFn(torch.autograd.Function):
         if n9 < g9.shape[1]:
             g9[:, n9:].zero_()
         wgrad(9, g9, ys[7], h, h)
-        g = dgrad(9, g9, h, mask=ys[7])       # G8
+        g = dgrad(9, g9, h, mask=8)       # G8
         for i in (8, 7):
             wgrad(i, g, ys[i - 2], h, h)
-            g = dgrad(i, g, h, mask=ys[i - 2])
+            g = dgrad(i, g, h, mask=i - 1)
         dx = torch.empty_like(x) if need_x else None
         wgrad(6, g, ys[4], h, h, x, ldx, pc)
-        g = dgrad(6, g, h, mask=ys[4], dx2=dx, p2=pc if need_x else 0)
+        g = dgrad(6, g, h, mask=5, dx2=dx, p2=pc if need_x else 0)
         for i in (5, 4, 3, 2):
             wgrad(i, g, ys[i - 2], h, h)
-            g = dgrad(i, g, h, mask=ys[i - 2])
+            g = dgrad(i, g, h, mask=i - 1)
         wgrad(1, g, x, ldx, pc)
         if need_x:
             dgrad(1, g, 0, dx2=dx, p2=pc, acc2=1)

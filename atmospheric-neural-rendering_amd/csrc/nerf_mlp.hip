@@ -39,106 +39,232 @@ struct NtArgs {
   const float* a1;
   const float* a2;
   int64_t lda1, lda2;
-  int32_t q1, q2;          // A's segment widths; Q = q1 + q2
+  int32_t q1, q2;          // A's segment widths; Q = q1 + q2 (q2 > 0: q1 % 16 == 0)
   const float* b;          // P x Q, row stride ldb
   int64_t ldb;
-  int64_t M;
-  int32_t P, p1;           // output columns; [0, p1) -> c1, [p1, P) -> c2
+  int64_t M;               // rows of this launch (A below 2^31 bytes: 32-bit offsets)
+  int32_t P, p1;           // output columns; [0, p1) -> c1, [p1, P) -> c2 (p1 % 64 == 0)
   float* c1;
   float* c2;
   int64_t ldc1, ldc2;
   const float* bias;       // P, or null
-  const float* mask;       // M x p1 (row stride ldm): zero the output where mask <= 0
-  int64_t ldm;
+  uint64_t* bits;          // forward: ReLU bitmask out (M x ceil(P / 64) words), or null
+  const uint64_t* mbits;   // input gradient: zero c1 where the bit is clear, or null
+  int32_t wpr;             // bitmask words per row
   int32_t relu, acc2;
 };
 
-// WR x WC waves per block, each owning a 64 x 64 output tile (4 x 4 MFMA tiles).
-template <int WR, int WC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+typedef uint32_t u4v __attribute__((vector_size(16)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, static_cast<int>(bytes),
+                                           0x00020000);
+}
+__device__ __forceinline__ f4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return f4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+            __uint_as_float(v[3])};
+}
+constexpr uint32_t kOob = 0x80000000u;  // past every num_records: the load returns zeros
+
+// WR x WC waves per block, each owning (16 TI) x (16 TJ) output tiles (TI x TJ MFMA
+// tiles), walking row tiles rt0, rt0 + stride, ... (persistent: the operand stream runs
+// on across tiles, so a tile's epilogue overlaps the next tile's first loads and a wave
+// pays its start-up latency once). The MFMA takes B as its A operand, so a lane's
+// accumulator holds four consecutive COLUMNS of one row (lane c, group g: row 16i + c,
+// columns 16j + 4g .. +3): the epilogue stores 16 B per lane. The main loop issues
+// nothing but the TI + TJ buffer loads and the 4 TI TJ MFMAs of a k-step: lane offsets
+// are fixed per tile (rows past M / columns past P are clamped onto real data, whose
+// results are never stored), the k offset rides in the scalar offset, and only a
+// segment's last, partial k-step zeroes lanes (B's, so the product vanishes whatever A
+// holds there). Two operand stages alternate by unrolling the k loop by 2. The ReLU mask
+// of the input-gradient epilogue is one bit per element, written by the forward (32x less
+// than re-reading the f32 activations) and loaded a k-step before the tile ends.
+template <int WR, int WC, int TI, int TJ, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 nt_kernel(NtArgs a) {
+  constexpr int RT = 16 * TI, CT = 16 * TJ;
+  constexpr int NW = (CT + 63) / 64;  // bitmask words a wave tile's row spans
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
-  const int64_t rb = (static_cast<int64_t>(blockIdx.x) * WR + wave / WC) * 64;
-  const int cb = (blockIdx.y * WC + wave % WC) * 64;
-  if (rb >= a.M || cb >= a.P) return;  // wave-uniform: no barrier below
-  const int Q = a.q1 + a.q2;
+  // the bias, read by the epilogue, in LDS (zeros past P)
+  __shared__ float sbias[16 * TJ * WC];
+  const int cb0 = blockIdx.y * WC * CT;
+  for (int e = threadIdx.x; e < 16 * TJ * WC; e += 256)
+    sbias[e] = a.bias && cb0 + e < a.P ? a.bias[cb0 + e] : 0.0f;
+  __syncthreads();
+  const int cb = (blockIdx.y * WC + wave % WC) * CT;
+  const int n_rt = static_cast<int>((a.M + RT - 1) / RT);
+  const int rt0 = blockIdx.x * WR + wave / WC;
+  const int rts = gridDim.x * WR;
+  if (rt0 >= n_rt || cb >= a.P) return;  // wave-uniform: no barrier below
+  const int s1steps = (a.q1 + 15) / 16;
+  // an even k-step count (a padding step reads B as zeros): the two operand stages
+  // alternate with no register copy at the tile seam
+  const int nsteps = (s1steps + (a.q2 + 15) / 16 + 1) & ~1;
+  const int Mi = static_cast<int>(a.M);
 
-  // the rows this lane loads (clamped; their results are not stored)
-  const float* ar1[4];
-  const float* ar2[4];
-  const float* br[4];
+  // each descriptor ends where its operand's last row does: a segment that starts inside
+  // a row (a view) must not reach past the allocation
+  const auto ra1 = rsrc(a.a1, ((a.M - 1) * a.lda1 + a.q1) * 4);
+  const auto ra2 = rsrc(a.a2, ((a.M - 1) * a.lda2 + (a.q2 ? a.q2 : a.q1)) * 4);
+  const auto rbm = rsrc(a.b, (static_cast<int64_t>(a.P - 1) * a.ldb + a.q1 + a.q2) * 4);
+  const uint32_t lda1b = static_cast<uint32_t>(a.lda1) * 4, lda2b = static_cast<uint32_t>(a.lda2) * 4;
+  const uint32_t ldbb = static_cast<uint32_t>(a.ldb) * 4;
+  uint32_t ob[TJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int64_t row = rb + 16 * i + c;
-    row = row < a.M ? row : a.M - 1;
-    ar1[i] = a.a1 + row * a.lda1;
-    ar2[i] = a.a2 + row * a.lda2 - a.q1;
-    int col = cb + 16 * i + c;
-    col = col < a.P ? col : a.P - 1;
-    br[i] = a.b + static_cast<int64_t>(col) * a.ldb;
+  for (int j = 0; j < TJ; ++j) {
+    const int col = min(cb + 16 * j + c, a.P - 1);
+    ob[j] = static_cast<uint32_t>(col) * ldbb + 16 * g;
   }
-  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-  auto load = [&](int k0, f4 (&av)[4], f4 (&bv)[4]) {
-    const int kk = k0 + 4 * g;
-    const bool ok = kk < Q;
-    const bool s1 = kk < a.q1;
+
+  struct Offs {
+    uint32_t a1[TI], a2[TI];
+  };
+  auto offsets = [&](int rt, Offs& o) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float* pa = s1 ? ar1[i] + kk : ar2[i] + kk;
-      av[i] = ok ? *reinterpret_cast<const f4*>(pa) : z4;
-      bv[i] = ok ? *reinterpret_cast<const f4*>(br[i] + kk) : z4;
+    for (int i = 0; i < TI; ++i) {
+      const uint32_t row = static_cast<uint32_t>(min(rt * RT + 16 * i + c, Mi - 1));
+      o.a1[i] = row * lda1b + 16 * g;
+      o.a2[i] = row * lda2b + 16 * g;
+    }
+  };
+  struct Stage {
+    f4 av[TI], bv[TJ];
+  };
+  const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+  auto load = [&](const Offs& o, int s, Stage& st) {
+    const bool seg1 = s < s1steps;
+    const int kl = seg1 ? 16 * s : 16 * (s - s1steps);
+    const uint32_t sa = static_cast<uint32_t>(kl) * 4;
+    const uint32_t sb = static_cast<uint32_t>(seg1 ? kl : a.q1 + kl) * 4;
+    const int qs = seg1 ? a.q1 : a.q2;
+    if (seg1) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) st.av[i] = bload4(ra1, o.a1[i], sa);
+    } else {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) st.av[i] = bload4(ra2, o.a2[i], sa);
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) st.bv[j] = bload4(rbm, ob[j], sb);
+    if (kl + 16 > qs) {  // the segment's partial last k-step (wave-uniform branch)
+      const bool ok = kl + 4 * g < qs;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) st.bv[j] = ok ? st.bv[j] : z4;
     }
   };
 
-  f4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = z4;
-
-  f4 an[4], bn[4];
-  load(0, an, bn);
-  for (int k0 = 0; k0 < Q; k0 += 16) {
-    f4 ac[4], bc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ac[i] = an[i];
-      bc[i] = bn[i];
-    }
-    if (k0 + 16 < Q) load(k0 + 16, an, bn);
+  f4 acc[TI][TJ];
+  auto mma = [&](const Stage& st) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(ac[i][t], bc[j][t], acc[i][j]);
-  }
+        for (int j = 0; j < TJ; ++j) acc[i][j] = mfma4(st.bv[j][t], st.av[i][t], acc[i][j]);
+  };
 
-  // epilogue: lane holds rows rb + 16i + 4g + r of column cb + 16j + c
+  // epilogue of row tile rt: lane holds row RT rt + 16i + c, columns cb + 16j + 4g .. +3;
+  // a column group that starts below P is stored whole (zeros past P: ldc >= round_up(P, 4))
+  // bitmask layout (private to the forward / input-gradient pair): in the 64-bit word of
+  // columns 64w .. 64w + 63, column 64w + 16j + 4g + r is bit 16g + 4j + r, so lane group
+  // g's 16 bits of a word are one contiguous u16
+  auto emit = [&](int row, int col, f4 v, uint32_t mnib) -> uint32_t {
+    if (row >= Mi || col >= a.P) return 0u;
+    const f4 bv = *reinterpret_cast<const f4*>(sbias + (col - cb0));
+    v += bv;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = cb + 16 * j + c;
-    if (col >= a.P) continue;
-    const float bias = a.bias ? a.bias[col] : 0.0f;
-    const bool seg1 = col < a.p1;
+    for (int r = 0; r < 4; ++r) {
+      if (a.relu) v[r] = v[r] > 0.0f ? v[r] : 0.0f;
+      if (col + r >= a.P) v[r] = 0.0f;
+    }
+    if (col < a.p1) {
+      if (a.mbits) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+        for (int r = 0; r < 4; ++r) v[r] = (mnib >> r) & 1u ? v[r] : 0.0f;
+      }
+      *reinterpret_cast<f4*>(a.c1 + static_cast<int64_t>(row) * a.ldc1 + col) = v;
+    } else {
+      f4* dst = reinterpret_cast<f4*>(a.c2 + static_cast<int64_t>(row) * a.ldc2 + (col - a.p1));
+      if (a.acc2) v += *dst;
+      *dst = v;
+    }
+    uint32_t nib = 0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = rb + 16 * i + 4 * g + r;
-        if (row >= a.M) continue;
-        float v = acc[i][j][r] + bias;
-        if (a.relu) v = v > 0.0f ? v : 0.0f;
-        if (seg1) {
-          if (a.mask && !(a.mask[row * a.ldm + col] > 0.0f)) v = 0.0f;
-          a.c1[row * a.ldc1 + col] = v;
-        } else {
-          float* dst = a.c2 + row * a.ldc2 + (col - a.p1);
-          *dst = a.acc2 ? *dst + v : v;
+    for (int r = 0; r < 4; ++r) nib |= (v[r] > 0.0f ? 1u : 0u) << r;
+    return nib;
+  };
+  // this lane's mask bits of the tile: row 16i + c, words cb/64 + w, the u16 of group g
+  uint16_t mw[TI][NW];
+  const uint16_t* mb16 = reinterpret_cast<const uint16_t*>(a.mbits);
+  auto load_mask = [&](int rt) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int row = rt * RT + 16 * i + c;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int wd = cb / 64 + w;
+        mw[i][w] = a.mbits && row < Mi && wd < a.wpr
+                       ? mb16[(static_cast<int64_t>(row) * a.wpr + wd) * 4 + g] : 0xFFFFu;
+      }
+    }
+  };
+  auto epilogue = [&](int rt) {
+    const int rowb = rt * RT;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int row = rowb + 16 * i + c;
+      uint64_t word[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) word[w] = 0;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int col = cb + 16 * j + 4 * g;
+        const int w = (16 * j) / 64, jw = j & 3;
+        const uint32_t nib = emit(row, col, acc[i][j], (mw[i][w] >> (4 * jw)) & 0xFu);
+        word[w] |= static_cast<uint64_t>(nib) << (16 * g + 4 * jw);
+      }
+      if (a.bits) {  // the four lane groups' nibbles of the row -> 64-bit words
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          uint32_t lo = static_cast<uint32_t>(word[w]), hi = static_cast<uint32_t>(word[w] >> 32);
+          lo |= __shfl_xor(lo, 16, 64);
+          hi |= __shfl_xor(hi, 16, 64);
+          lo |= __shfl_xor(lo, 32, 64);
+          hi |= __shfl_xor(hi, 32, 64);
+          const int wd = cb / 64 + w;
+          if (g == 0 && row < Mi && wd < a.wpr)
+            a.bits[static_cast<int64_t>(row) * a.wpr + wd] = (static_cast<uint64_t>(hi) << 32) | lo;
         }
       }
     }
+  };
+
+  Offs ocur;
+  offsets(rt0, ocur);
+  Stage A, B;
+  load(ocur, 0, A);
+  for (int rt = rt0; rt < n_rt; rt += rts) {
+    const bool more = rt + rts < n_rt;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = z4;
+    // invariant: A holds k-step s of this tile
+    for (int s = 0; s < nsteps; s += 2) {
+      load(ocur, s + 1, B);
+      if (s + 2 == nsteps) load_mask(rt);
+      mma(A);
+      if (s + 2 < nsteps) {
+        load(ocur, s + 2, A);
+      } else if (more) {
+        offsets(rt + rts, ocur);
+        load(ocur, 0, A);
+      }
+      mma(B);
+    }
+    epilogue(rt);
   }
 }
 
@@ -177,12 +303,25 @@ dw_kernel(DwArgs a) {
   int64_t m_end = m_begin + wrows;
   m_end = m_end < a.M ? m_end : a.M;
 
+  // buffer loads: the lane's offsets within a row are fixed, the row advance rides in the
+  // scalar offset, and the descriptors end at this wave's last row (rows past it read
+  // zeros). Columns past the operand's width read real data of the same arrays, whose
+  // results (partial rows n >= N, columns k >= K) are never summed.
   const int n4 = nb + 4 * c, k4 = kb + 4 * c;
-  const bool gok = n4 < a.Nr;
-  const bool xok = k4 < K;
-  const float* gcol = a.g + n4;
-  const float* xcol = k4 < a.q1 ? a.a1 + k4 : a.a2 + (k4 - a.q1);
-  const int64_t ldx = k4 < a.q1 ? a.lda1 : a.lda2;
+  const bool seg1 = kb < a.q1;  // host: q1 % 64 == 0 when q2 > 0, so uniform per block
+  const float* xb = seg1 ? a.a1 : a.a2;
+  const uint32_t ldx4 = static_cast<uint32_t>(seg1 ? a.lda1 : a.lda2) * 4;
+  const uint32_t ldg4 = static_cast<uint32_t>(a.ldg) * 4;
+  const int xcol = seg1 ? k4 : k4 - a.q1;
+  // the descriptors end at the wave's last row, at its last column of the operand
+  const auto rg = rsrc(a.g, ((m_end - 1) * a.ldg + a.Nr) * 4);
+  const auto rx = rsrc(xb, ((m_end - 1) * (seg1 ? a.lda1 : a.lda2) + (seg1 ? a.q1 : a.q2)) * 4);
+  uint32_t vg[4], vx[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    vg[t] = static_cast<uint32_t>(4 * g + t) * ldg4 + static_cast<uint32_t>(n4) * 4;
+    vx[t] = static_cast<uint32_t>(4 * g + t) * ldx4 + static_cast<uint32_t>(xcol) * 4;
+  }
   const bool do_db = blockIdx.y == 0;
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
 
@@ -193,34 +332,38 @@ dw_kernel(DwArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = z4;
   f4 dbacc = z4;
 
-  auto load = [&](int64_t m0, f4 (&gv)[4], f4 (&xv)[4]) {
+  struct Stage {
+    f4 gv[4], xv[4];
+  };
+  auto load = [&](int64_t m0, Stage& st) {
+    const uint32_t sg = static_cast<uint32_t>(m0) * ldg4, sx = static_cast<uint32_t>(m0) * ldx4;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int64_t m = m0 + 4 * g + t;
-      const bool ok = m < m_end;
-      gv[t] = ok && gok ? *reinterpret_cast<const f4*>(gcol + m * a.ldg) : z4;
-      xv[t] = ok && xok ? *reinterpret_cast<const f4*>(xcol + m * ldx) : z4;
+      st.gv[t] = bload4(rg, vg[t], sg);
+      st.xv[t] = bload4(rx, vx[t], sx);
+    }
+  };
+  auto mma = [&](const Stage& st) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(st.gv[t][i], st.xv[t][j], acc[i][j]);
+      if (do_db) dbacc += st.gv[t];
     }
   };
   if (m_begin < m_end) {
-    f4 gn[4], xn[4];
-    load(m_begin, gn, xn);
-    for (int64_t m0 = m_begin; m0 < m_end; m0 += 16) {
-      f4 gc[4], xc[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        gc[t] = gn[t];
-        xc[t] = xn[t];
-      }
-      if (m0 + 16 < m_end) load(m0 + 16, gn, xn);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(gc[t][i], xc[t][j], acc[i][j]);
-        if (do_db) dbacc += gc[t];
-      }
+    // an even number of 16-row steps (a padding step past m_end reads zeros)
+    const int nst = (static_cast<int>((m_end - m_begin + 15) / 16) + 1) & ~1;
+    Stage A, B;
+    load(m_begin, A);
+    for (int st = 0; st < nst; st += 2) {
+      const int64_t m0 = m_begin + 16LL * st;
+      load(m0 + 16, B);
+      mma(A);
+      if (st + 2 < nst) load(m0 + 32, A);
+      mma(B);
     }
   }
 
@@ -285,6 +428,68 @@ __global__ void __launch_bounds__(256) dw_reduce_kernel(const float* __restrict_
   }
 }
 
+// M in chunks whose A operands stay below 2^31 bytes (32-bit buffer offsets); a
+// persistent grid of 1,024 blocks walks each chunk's row tiles with 64 x 64 wave tiles
+// (two waves per SIMD). (128 x 128 wave tiles, 256 accumulators at one wave per SIMD,
+// were tried: the compiler spills 56-270 VGPRs for them.)
+template <int WR, int WC, int TI, int TJ, int WPE>
+static void launch_cfg(const NtArgs& a, int64_t blocks_cap, hipStream_t st) {
+  const int64_t rows = 16LL * TI * WR;
+  const unsigned gy = static_cast<unsigned>(ceil_div(a.P, 16LL * TJ * WC));
+  int64_t gx = ceil_div(a.M, rows);
+  const int64_t cap = ceil_div(blocks_cap, gy);
+  gx = gx < cap ? gx : cap;
+  nt_kernel<WR, WC, TI, TJ, WPE><<<dim3(static_cast<unsigned>(gx), gy), 256, 0, st>>>(a);
+}
+
+static void launch_nt(NtArgs a, hipStream_t st) {
+  const int64_t ld = a.lda1 > a.lda2 ? a.lda1 : a.lda2;
+  const int64_t chunk = ((0x7fffffffLL / (ld * 4)) / 256) * 256;
+  const int64_t M = a.M;
+  for (int64_t r0 = 0; r0 < M; r0 += chunk) {
+    NtArgs b = a;
+    b.M = M - r0 < chunk ? M - r0 : chunk;
+    b.a1 = a.a1 + r0 * a.lda1;
+    b.a2 = a.a2 + r0 * a.lda2;
+    b.c1 = a.c1 + r0 * a.ldc1;
+    b.c2 = a.c2 + r0 * a.ldc2;
+    if (a.bits) b.bits = a.bits + r0 * a.wpr;
+    if (a.mbits) b.mbits = a.mbits + r0 * a.wpr;
+    if (a.P <= 128) {
+      launch_cfg<2, 2, 4, 4, 2>(b, 1024, st);
+      continue;
+    }
+    // the first 256 columns with four 64-wide column waves per block; columns past 256
+    // (fc9's density outputs, fc6's skip input gradient) in a second launch of blocks
+    // with two column waves, rather than a second block column that leaves 2-3 of its
+    // four waves idle
+    NtArgs m = b;
+    m.P = a.P < 256 ? a.P : 256;
+    m.p1 = a.p1 < m.P ? a.p1 : m.P;
+    launch_cfg<1, 4, 4, 4, 2>(m, 1024, st);
+    if (a.P > 256) {
+      NtArgs t = b;
+      t.P = a.P - 256;
+      t.b = b.b + 256 * b.ldb;
+      if (b.bias) t.bias = b.bias + 256;
+      if (a.p1 > 256) {
+        t.p1 = a.p1 - 256;
+        t.c1 = b.c1 + 256;
+        t.c2 = b.c2;
+      } else {
+        t.p1 = 0;
+        t.c1 = b.c2 + (256 - a.p1);
+        t.c2 = b.c2 + (256 - a.p1);
+        t.ldc1 = b.ldc2;
+        t.mbits = nullptr;
+      }
+      if (b.bits) t.bits = b.bits + 4;
+      if (t.mbits) t.mbits = b.mbits + 4;
+      launch_cfg<2, 2, 4, 4, 2>(t, 1024, st);
+    }
+  }
+}
+
 struct DwGeom {
   int32_t tn, tk, S;
   int64_t rows_per_block;
@@ -315,15 +520,17 @@ using namespace anr::nerfmlp;
 extern "C" int anr_nerf_linear_fwd(const float* a1, int64_t lda1, int32_t q1, const float* a2,
                                    int64_t lda2, int32_t q2, int64_t M, const float* w,
                                    int32_t n, const float* bias, int32_t relu, float* y,
-                                   int64_t ldy, anr_stream_t stream) {
+                                   int64_t ldy, uint64_t* relu_bits, anr_stream_t stream) {
   ANR_CHECK_ARG(M >= 0 && n > 0 && q1 > 0 && q2 >= 0, "anr_nerf_linear_fwd: bad sizes");
+  if (M == 0) return ANR_OK;  // empty tensors carry null pointers
   ANR_CHECK_ARG(q1 % 4 == 0 && q2 % 4 == 0 && lda1 % 4 == 0 && (q2 == 0 || lda2 % 4 == 0),
                 "anr_nerf_linear_fwd: segment widths and strides must be multiples of 4");
-  ANR_CHECK_ARG(lda1 >= q1 && (q2 == 0 || lda2 >= q2) && ldy >= n,
-                "anr_nerf_linear_fwd: strides below the widths");
-  ANR_CHECK_ARG(al16(a1) && (q2 == 0 || al16(a2)) && al16(w) && a1 && w && y,
+  ANR_CHECK_ARG(lda1 >= q1 && (q2 == 0 || lda2 >= q2) && ldy % 4 == 0 && ldy >= (n + 3) / 4 * 4,
+                "anr_nerf_linear_fwd: strides below the widths (ldy: round_up(n, 4))");
+  ANR_CHECK_ARG(q2 == 0 || q1 % 16 == 0,
+                "anr_nerf_linear_fwd: with a second segment q1 must be a multiple of 16");
+  ANR_CHECK_ARG(al16(a1) && (q2 == 0 || al16(a2)) && al16(w) && al16(y) && a1 && w && y,
                 "anr_nerf_linear_fwd: operands must be 16-byte aligned");
-  if (M == 0) return ANR_OK;
   NtArgs a{};
   a.a1 = a1;
   a.a2 = q2 ? a2 : a1;
@@ -341,32 +548,31 @@ extern "C" int anr_nerf_linear_fwd(const float* a1, int64_t lda1, int32_t q1, co
   a.ldc1 = a.ldc2 = ldy;
   a.bias = bias;
   a.relu = relu;
-  hipStream_t st = as_stream(stream);
-  if (n > 128) {
-    dim3 grid(static_cast<unsigned>(ceil_div(M, 64)), static_cast<unsigned>(ceil_div(n, 256)));
-    nt_kernel<1, 4><<<grid, 256, 0, st>>>(a);
-  } else {
-    dim3 grid(static_cast<unsigned>(ceil_div(M, 128)), static_cast<unsigned>(ceil_div(n, 128)));
-    nt_kernel<2, 2><<<grid, 256, 0, st>>>(a);
-  }
+  a.bits = relu_bits;
+  a.wpr = static_cast<int32_t>((n + 63) / 64);
+  launch_nt(a, as_stream(stream));
   ANR_CHECK_LAUNCH("anr_nerf_linear_fwd");
   return ANR_OK;
 }
 
 extern "C" int anr_nerf_linear_dx(const float* g, int64_t ldg, int64_t M, int32_t n,
                                   const float* wt, int64_t ldwt, int32_t p1, int32_t p2,
-                                  const float* mask, int64_t ldm, float* dx1, int64_t ldx1,
+                                  const uint64_t* mask_bits, float* dx1, int64_t ldx1,
                                   float* dx2, int64_t ldx2, int32_t acc2,
                                   anr_stream_t stream) {
   ANR_CHECK_ARG(M >= 0 && n > 0 && p1 >= 0 && p2 >= 0 && p1 + p2 > 0,
                 "anr_nerf_linear_dx: bad sizes");
+  if (M == 0) return ANR_OK;  // empty tensors carry null pointers
   ANR_CHECK_ARG(ldg % 4 == 0 && ldwt % 4 == 0 && ldg >= n && ldwt >= n,
                 "anr_nerf_linear_dx: G and W^T row strides must be multiples of 4 >= n");
   ANR_CHECK_ARG(al16(g) && al16(wt) && g && wt && (p1 == 0 || dx1) && (p2 == 0 || dx2),
                 "anr_nerf_linear_dx: operands must be 16-byte aligned");
-  ANR_CHECK_ARG((p1 == 0 || ldx1 >= p1) && (p2 == 0 || ldx2 >= p2) && (!mask || ldm >= p1),
+  ANR_CHECK_ARG((p1 == 0 || ldx1 >= p1) && (p2 == 0 || ldx2 >= p2),
                 "anr_nerf_linear_dx: strides below the widths");
-  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(p1 % 64 == 0 && p2 % 4 == 0 && (p1 == 0 || (ldx1 % 4 == 0 && al16(dx1))) &&
+                    (p2 == 0 || (ldx2 % 4 == 0 && al16(dx2))),
+                "anr_nerf_linear_dx: p1 must be a multiple of 64, p2 of 4, the outputs "
+                "16-byte granular");
   // the contraction runs over n rounded up to 4: G's pad columns and W^T's are zero
   NtArgs a{};
   a.a1 = a.a2 = g;
@@ -382,19 +588,11 @@ extern "C" int anr_nerf_linear_dx(const float* g, int64_t ldg, int64_t M, int32_
   a.c2 = p2 ? dx2 : dx1;
   a.ldc1 = p1 ? ldx1 : ldx2;
   a.ldc2 = p2 ? ldx2 : ldx1;
-  a.mask = mask;
-  a.ldm = ldm;
+  a.mbits = p1 ? mask_bits : nullptr;
+  a.wpr = static_cast<int32_t>((p1 + 63) / 64);
   a.acc2 = acc2;
   ANR_CHECK_ARG(a.q1 <= ldg && a.q1 <= ldwt, "anr_nerf_linear_dx: pad columns missing");
-  hipStream_t st = as_stream(stream);
-  const int P = p1 + p2;
-  if (P > 128) {
-    dim3 grid(static_cast<unsigned>(ceil_div(M, 64)), static_cast<unsigned>(ceil_div(P, 256)));
-    nt_kernel<1, 4><<<grid, 256, 0, st>>>(a);
-  } else {
-    dim3 grid(static_cast<unsigned>(ceil_div(M, 128)), static_cast<unsigned>(ceil_div(P, 128)));
-    nt_kernel<2, 2><<<grid, 256, 0, st>>>(a);
-  }
+  launch_nt(a, as_stream(stream));
   ANR_CHECK_LAUNCH("anr_nerf_linear_dx");
   return ANR_OK;
 }
@@ -411,40 +609,50 @@ extern "C" int anr_nerf_linear_dw(const float* g, int64_t ldg, int64_t M, int32_
                                   int64_t lda2, int32_t q2, float* dw, float* db, void* ws,
                                   int64_t ws_bytes, anr_stream_t stream) {
   ANR_CHECK_ARG(M >= 0 && n > 0 && q1 > 0 && q2 >= 0, "anr_nerf_linear_dw: bad sizes");
+  if (M == 0) return ANR_OK;  // empty tensors carry null pointers
+  ANR_CHECK_ARG(q2 == 0 || q1 % 64 == 0,
+                "anr_nerf_linear_dw: with a second segment q1 must be a multiple of 64");
   ANR_CHECK_ARG(q1 % 4 == 0 && q2 % 4 == 0 && lda1 % 4 == 0 && (q2 == 0 || lda2 % 4 == 0) &&
                     ldg % 4 == 0 && ldg >= (n + 3) / 4 * 4,
                 "anr_nerf_linear_dw: widths and strides must be multiples of 4 (G padded)");
   ANR_CHECK_ARG(al16(g) && al16(a1) && (q2 == 0 || al16(a2)) && al16(ws) && dw,
                 "anr_nerf_linear_dw: operands must be 16-byte aligned");
-  if (M == 0) return ANR_OK;
   const int32_t K = q1 + q2;
-  const DwGeom d = dw_geom(M, n, K);
   ANR_CHECK_ARG(ws_bytes >= anr_nerf_linear_dw_workspace(M, n, K),
                 "anr_nerf_linear_dw: workspace of %lld bytes < %lld", (long long)ws_bytes,
                 (long long)anr_nerf_linear_dw_workspace(M, n, K));
-  DwArgs a{};
-  a.g = g;
-  a.ldg = ldg;
-  a.Nr = (n + 3) / 4 * 4;
-  a.a1 = a1;
-  a.a2 = q2 ? a2 : a1;
-  a.lda1 = lda1;
-  a.lda2 = q2 ? lda2 : lda1;
-  a.q1 = q1;
-  a.q2 = q2;
-  a.M = M;
-  a.rows_per_block = d.rows_per_block;
-  a.Np = 64 * d.tn;
-  a.Kp = 64 * d.tk;
-  a.part = static_cast<float*>(ws);
-  a.dbpart = a.part + static_cast<int64_t>(d.S) * a.Np * a.Kp;
+  // rows in chunks whose operands stay below 2^31 bytes (32-bit buffer offsets); every
+  // chunk adds its own partial sums into dw / db
+  int64_t ldmax = ldg > lda1 ? ldg : lda1;
+  if (q2 && lda2 > ldmax) ldmax = lda2;
+  const int64_t chunk = ((0x7fffffffLL / (ldmax * 4)) / 64) * 64;
   hipStream_t st = as_stream(stream);
-  dim3 grid(static_cast<unsigned>(d.tn), static_cast<unsigned>(d.tk), static_cast<unsigned>(d.S));
-  dw_kernel<<<grid, 256, 0, st>>>(a);
-  ANR_CHECK_LAUNCH("anr_nerf_linear_dw");
-  const int64_t total = static_cast<int64_t>(n) * K + (db ? n : 0);
-  dw_reduce_kernel<<<static_cast<unsigned>(ceil_div(total, 256)), 256, 0, st>>>(
-      a.part, a.dbpart, d.S, n, K, a.Np, a.Kp, dw, db);
-  ANR_CHECK_LAUNCH("anr_nerf_linear_dw (reduce)");
+  for (int64_t r0 = 0; r0 < M; r0 += chunk) {
+    const int64_t Mc = M - r0 < chunk ? M - r0 : chunk;
+    const DwGeom d = dw_geom(Mc, n, K);
+    DwArgs a{};
+    a.g = g + r0 * ldg;
+    a.ldg = ldg;
+    a.Nr = (n + 3) / 4 * 4;
+    a.a1 = a1 + r0 * lda1;
+    a.a2 = q2 ? a2 + r0 * lda2 : a.a1;
+    a.lda1 = lda1;
+    a.lda2 = q2 ? lda2 : lda1;
+    a.q1 = q1;
+    a.q2 = q2;
+    a.M = Mc;
+    a.rows_per_block = d.rows_per_block;
+    a.Np = 64 * d.tn;
+    a.Kp = 64 * d.tk;
+    a.part = static_cast<float*>(ws);
+    a.dbpart = a.part + static_cast<int64_t>(d.S) * a.Np * a.Kp;
+    dim3 grid(static_cast<unsigned>(d.tn), static_cast<unsigned>(d.tk), static_cast<unsigned>(d.S));
+    dw_kernel<<<grid, 256, 0, st>>>(a);
+    ANR_CHECK_LAUNCH("anr_nerf_linear_dw");
+    const int64_t total = static_cast<int64_t>(n) * K + (db ? n : 0);
+    dw_reduce_kernel<<<static_cast<unsigned>(ceil_div(total, 256)), 256, 0, st>>>(
+        a.part, a.dbpart, d.S, n, K, a.Np, a.Kp, dw, db);
+    ANR_CHECK_LAUNCH("anr_nerf_linear_dw (reduce)");
+  }
   return ANR_OK;
 }

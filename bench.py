@@ -304,7 +304,7 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
     flops = 3.0 * (nerf_mlp_flops(pipe.nerf["coarse"], batch_size * nc)
                    + nerf_mlp_flops(pipe.nerf["fine"], batch_size * (nc + nf)))
     tfs = flops / (ms * 1e-3) / 1e12
-    from atmonr_amd import nerf_model
+    from atmonr_amd import _lib, nerf_model
 
     native = nerf_model._NATIVE
     roofline = {"kernel": ("nerf_linear_{fwd,dx,dw} (csrc/nerf_mlp.hip f32 MFMA GEMMs), "

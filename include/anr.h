@@ -412,22 +412,28 @@ int anr_relu_bwd_colsum(const float* g, const float* y, int64_t M, int32_t C, fl
  * autograd backward. Operands are row-major f32 with 16-byte-aligned rows: every leading
  * dimension and segment width is a multiple of 4.
  *
- * Forward: y (M x n, row stride ldy) = [a1 | a2] W^T + bias, then ReLU if relu != 0.
- *   a1 is M x q1 and a2 is M x q2 (q2 = 0: none); they are the fc6 skip and fc10
- *   direction concats, read in place. W is n x (q1+q2), as nn.Linear.weight. bias is
- *   nullable. */
+ * Forward: y (M x n, row stride ldy >= round_up(n, 4)) = [a1 | a2] W^T + bias, then ReLU
+ * if relu != 0. Columns n .. round_up(n, 4) come out zero.
+ *   a1 is M x q1 and a2 is M x q2 (q2 = 0: none; q1 % 16 == 0 when q2 > 0). They are the
+ *   fc6 skip and fc10 direction concats, read in place.
+ *   W is n x (q1+q2), as nn.Linear.weight. bias is nullable.
+ *   relu_bits is nullable. If given, it receives M x ceil(n/64) 64-bit words, one bit
+ *   per element: y[m][64w + 16j + 4g + r] > 0 is bit 16g + 4j + r of word w of row m.
+ *   That is the ReLU mask for the layer's backward, 32x smaller than the activations. */
 int anr_nerf_linear_fwd(const float* a1, int64_t lda1, int32_t q1, const float* a2,
                         int64_t lda2, int32_t q2, int64_t M, const float* w, int32_t n,
                         const float* bias, int32_t relu, float* y, int64_t ldy,
-                        anr_stream_t stream);
+                        uint64_t* relu_bits, anr_stream_t stream);
 /* Input gradient: [dx1 | dx2] (M x (p1+p2)) = g (M x n) W, with wt = W^T
  * ((p1+p2) x n, row stride ldwt).
+ *   p1 % 64 == 0 and p2 % 4 == 0.
  *   If n % 4 != 0, g's and wt's columns n .. round_up(n, 4) must exist and be zero.
- *   dx1 (first p1 columns) is zeroed where mask (M x p1, nullable) is <= 0. That is the
- *   ReLU backward of the layer whose output the input was.
+ *   dx1 (first p1 columns) is zeroed where the bit in mask_bits is clear. mask_bits is
+ *   the relu_bits of the forward that produced the input, M x ceil(p1/64) words, or
+ *   NULL for no mask. This is the ReLU backward of the layer below.
  *   dx2 (last p2 columns) is written, or added to if acc2 != 0. */
 int anr_nerf_linear_dx(const float* g, int64_t ldg, int64_t M, int32_t n, const float* wt,
-                       int64_t ldwt, int32_t p1, int32_t p2, const float* mask, int64_t ldm,
+                       int64_t ldwt, int32_t p1, int32_t p2, const uint64_t* mask_bits,
                        float* dx1, int64_t ldx1, float* dx2, int64_t ldx2, int32_t acc2,
                        anr_stream_t stream);
 /* Parameter gradients, ACCUMULATED: dw (n x (q1+q2), contiguous) += g^T [a1 | a2], and

@@ -283,10 +283,26 @@ def _f32_bar(a, b):
     return 2e-5 * (a.double().abs() @ b.double().abs().t()) + 1e-30
 
 
+def _pack_bits(mask):
+    """(M, C) bool -> (M, ceil(C/64)) int64 words in the kernels' layout: column
+    64w + 16j + 4g + r is bit 16g + 4j + r of word w (csrc/nerf_mlp.hip)."""
+    M, C = mask.shape
+    W = (C + 63) // 64
+    m = torch.zeros(M, W * 64, dtype=torch.int64, device=mask.device)
+    m[:, :C] = mask.long()
+    k = torch.arange(64, device=mask.device, dtype=torch.int64)
+    j, g, r = k // 16, (k % 16) // 4, k % 4
+    shifts = 16 * g + 4 * j + r
+    return (m.view(M, W, 64) << shifts).sum(-1)
+
+
 @pytest.mark.parametrize("M,q1,q2,n,relu", [(1000, 76, 0, 256, 1), (4096, 256, 76, 256, 1),
                                             (777, 256, 24, 128, 1), (300, 256, 0, 257, 0),
-                                            (64, 128, 0, 4, 0), (0, 256, 0, 256, 1)])
+                                            (64, 128, 0, 4, 0), (70000, 256, 0, 256, 1),
+                                            (0, 256, 0, 256, 1)])
 def test_nerf_linear_fwd_matches_f64(dev, M, q1, q2, n, relu):
+    """Y = [A1 | A2] W^T + b (+ ReLU), the pad columns zero, and the ReLU bitmask equal to
+    (Y > 0) bit for bit."""
     from atmonr_amd import _lib
 
     gen = torch.Generator(device=dev).manual_seed(M + n)
@@ -296,23 +312,28 @@ def test_nerf_linear_fwd_matches_f64(dev, M, q1, q2, n, relu):
     b = torch.randn(n, device=dev, generator=gen)
     ld = (n + 3) // 4 * 4
     y = torch.full((M, ld), float("nan"), device=dev)
+    bits = torch.full((M, (n + 63) // 64), -1, dtype=torch.int64, device=dev) if relu else None
     a2 = x[:, q1:] if q2 else None
     _lib.call("anr_nerf_linear_fwd", _lib.ptr(x), lda, q1, _lib.ptr(a2), lda, q2, M,
-              _lib.ptr(w), n, _lib.ptr(b), relu, _lib.ptr(y), ld, _lib.stream(dev))
+              _lib.ptr(w), n, _lib.ptr(b), relu, _lib.ptr(y), ld, _lib.ptr(bits),
+              _lib.stream(dev))
     a = x[:, : q1 + q2]
     want = a.double() @ w.double().t() + b.double()
     bar = _f32_bar(a, w) + 1e-6 * b.double().abs()
     if relu:
         want = want.clamp_min(0)
     assert torch.all((y[:, :n].double() - want).abs() <= bar)
+    assert torch.all(y[:, n:] == 0)
+    if relu:
+        assert torch.equal(bits, _pack_bits(y[:, :n] > 0))
 
 
 @pytest.mark.parametrize("M,n,p1,p2,acc2", [(1000, 256, 256, 76, 0), (1000, 256, 0, 76, 1),
                                             (555, 257, 256, 0, 0), (300, 4, 128, 0, 0),
-                                            (4096, 128, 0, 256, 0)])
+                                            (4096, 128, 0, 256, 0), (70001, 256, 256, 0, 0)])
 def test_nerf_linear_dx_matches_f64(dev, M, n, p1, p2, acc2):
-    """dX = G W with the ReLU mask of the saved input on the first p1 columns (exactly
-    torch's threshold_backward) and an accumulating second segment."""
+    """dX = G W with the ReLU bitmask applied to the first p1 columns (exactly zero where
+    the bit is clear, as torch's threshold_backward) and an accumulating second segment."""
     from atmonr_amd import _lib
 
     gen = torch.Generator(device=dev).manual_seed(M + n + p1)
@@ -322,20 +343,21 @@ def test_nerf_linear_dx_matches_f64(dev, M, n, p1, p2, acc2):
     w = torch.randn(n, p1 + p2, device=dev, generator=gen) * 0.1
     wt = torch.zeros(p1 + p2, nr, device=dev)
     wt[:, :n] = w.t()
-    mask = torch.relu(torch.randn(M, max(p1, 1), device=dev, generator=gen))
+    keep = torch.rand(M, max(p1, 1), device=dev, generator=gen) > 0.4
+    bits = _pack_bits(keep[:, :p1]) if p1 else None
     dx1 = torch.full((M, max(p1, 1)), float("nan"), device=dev)
     base = torch.randn(M, p2 + 4, device=dev, generator=gen)
     dx2 = base.clone()
     _lib.call("anr_nerf_linear_dx", _lib.ptr(g), nr, M, n, _lib.ptr(wt), nr, p1, p2,
-              _lib.ptr(mask) if p1 else None, mask.stride(0), _lib.ptr(dx1) if p1 else None,
-              dx1.stride(0), _lib.ptr(dx2) if p2 else None, dx2.stride(0), acc2,
-              _lib.stream(dev))
+              _lib.ptr(bits), _lib.ptr(dx1) if p1 else None, dx1.stride(0),
+              _lib.ptr(dx2) if p2 else None, dx2.stride(0), acc2, _lib.stream(dev))
     full = g[:, :n].double() @ w.double()
     bar = _f32_bar(g[:, :n], w.t())
     if p1:
-        want = torch.where(mask[:, :p1] > 0, full[:, :p1], torch.zeros_like(full[:, :p1]))
+        k = keep[:, :p1]
+        want = torch.where(k, full[:, :p1], torch.zeros_like(full[:, :p1]))
         assert torch.all((dx1[:, :p1].double() - want).abs() <= bar[:, :p1])
-        assert torch.equal(dx1[:, :p1][mask[:, :p1] <= 0], torch.zeros_like(dx1[:, :p1][mask[:, :p1] <= 0]))
+        assert torch.all(dx1[:, :p1][~k] == 0)
     if p2:
         want2 = full[:, p1:] + (base[:, :p2].double() if acc2 else 0)
         assert torch.all((dx2[:, :p2].double() - want2).abs()
@@ -410,7 +432,15 @@ def test_atmonerf_native_matches_library_path(dev, vol, M):
     (cn, sn, xn, gn), (ct, s_t, xt, gt) = res["native"], res["torch"]
     close(cn, ct, rel=1e-4, atol=1e-6, what="color")
     close(sn, s_t, rel=1e-4, atol=1e-5, what="sigma")
+
+    def rel_l2(a, b):
+        return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+    # gradients: relative L2. A pre-activation within f32 rounding of 0 can take the
+    # ReLU's other branch in the two summation orders, which moves that row's backward
+    # by O(|g w|): elementwise bars would test the branch, not the kernels (measured on
+    # MI355X: one dL/dx element 3e-2 apart on a max of 4.4 at 8,199 rows)
     # the direction columns are data: the native path leaves their gradient zero
-    close(xn[:, :76], xt[:, :76], rel=1e-3, atol=1e-6, what="dL/dx_pos")
-    for i, (a, b) in enumerate(zip(gn, gt)):
-        close(a, b, rel=1e-3, atol=1e-6, what=f"param {i}")
+    errs = [rel_l2(xn[:, :76], xt[:, :76])] + [rel_l2(a, b) for a, b in zip(gn, gt)]
+    print("rel L2 dx_pos, params:", ["%.2e" % e for e in errs])
+    assert max(errs) <= 1e-3, errs

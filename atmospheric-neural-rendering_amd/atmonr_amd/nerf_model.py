@@ -349,7 +349,9 @@ class AtmoNeRF(nn.Module):
     def forward(self, x: torch.Tensor, noise: torch.Tensor | None = None):
         """models/nerf.py:73-93: (sigmoid color, sigma). fc9's hidden part feeds fc10
         without an activation, as in the reference."""
-        if _native_ok(x) and x.shape[1] == self.pos_channels + self.dir_channels:
+        if (_native_ok(x) and x.shape[1] == self.pos_channels + self.dir_channels
+                and self.hidden_dim % 64 == 0 and self.pos_channels % 4 == 0
+                and self.dir_channels % 4 == 0):
             if self.training and noise is None:
                 noise = torch.randn(x.shape[0], self.volume_channels, device=x.device)
             return _AtmoNeRFFn.apply(x, noise if self.training else None, self,

@@ -43,7 +43,7 @@ struct NtArgs {
   const float* b;          // P x Q, row stride ldb
   int64_t ldb;
   int64_t M;               // rows of this launch (A below 2^31 bytes: 32-bit offsets)
-  int32_t P, p1;           // output columns; [0, p1) -> c1, [p1, P) -> c2 (p1 % 64 == 0)
+  int32_t P, p1;           // output columns; [0, p1) -> c1, [p1, P) -> c2 (p1 % 4 == 0)
   float* c1;
   float* c2;
   int64_t ldc1, ldc2;
@@ -569,10 +569,10 @@ extern "C" int anr_nerf_linear_dx(const float* g, int64_t ldg, int64_t M, int32_
                 "anr_nerf_linear_dx: operands must be 16-byte aligned");
   ANR_CHECK_ARG((p1 == 0 || ldx1 >= p1) && (p2 == 0 || ldx2 >= p2),
                 "anr_nerf_linear_dx: strides below the widths");
-  ANR_CHECK_ARG(p1 % 64 == 0 && p2 % 4 == 0 && (p1 == 0 || (ldx1 % 4 == 0 && al16(dx1))) &&
+  ANR_CHECK_ARG(p1 % 4 == 0 && p2 % 4 == 0 && (p1 == 0 || (ldx1 % 4 == 0 && al16(dx1))) &&
                     (p2 == 0 || (ldx2 % 4 == 0 && al16(dx2))),
-                "anr_nerf_linear_dx: p1 must be a multiple of 64, p2 of 4, the outputs "
-                "16-byte granular");
+                "anr_nerf_linear_dx: p1 and p2 must be multiples of 4, the outputs 16-byte "
+                "granular");
   // the contraction runs over n rounded up to 4: G's pad columns and W^T's are zero
   NtArgs a{};
   a.a1 = a.a2 = g;

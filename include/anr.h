@@ -426,7 +426,7 @@ int anr_nerf_linear_fwd(const float* a1, int64_t lda1, int32_t q1, const float* 
                         uint64_t* relu_bits, anr_stream_t stream);
 /* Input gradient: [dx1 | dx2] (M x (p1+p2)) = g (M x n) W, with wt = W^T
  * ((p1+p2) x n, row stride ldwt).
- *   p1 % 64 == 0 and p2 % 4 == 0.
+ *   p1 % 4 == 0 and p2 % 4 == 0.
  *   If n % 4 != 0, g's and wt's columns n .. round_up(n, 4) must exist and be zero.
  *   dx1 (first p1 columns) is zeroed where the bit in mask_bits is clear. mask_bits is
  *   the relu_bits of the forward that produced the input, M x ceil(p1/64) words, or

@@ -31,6 +31,35 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
+// The GEMM loops accumulate in AGPRs (as tuned library kernels do) through inline asm: the
+// builtin lets the compiler keep the accumulators in VGPRs. "s_nop 1" covers the VALU
+// write -> MFMA read wait states of operands a zeroing select just wrote (the compiler
+// pads nothing inside an asm statement); the accumulators are read back only after
+// acc_fence() + acc_pin(), which cover the result latency (40 cycles for this shape).
+#ifndef NERF_AGPR
+#define NERF_AGPR 1
+#endif
+__device__ __forceinline__ void mfma4_acc(f4& acc, float a, float b) {
+#if NERF_AGPR
+  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+#else
+  acc = mfma4(a, b, acc);
+#endif
+}
+__device__ __forceinline__ void acc_fence() {
+#if NERF_AGPR
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#endif
+}
+template <int N, int K>
+__device__ __forceinline__ void acc_pin(f4 (&acc)[N][K]) {
+#if NERF_AGPR
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < K; ++j) asm volatile("" : "+a"(acc[i][j]));
+#endif
+}
 
 // ---------------------------------------------------------------------------------
 // C (M x P) = A (M x Q, two column segments) . B^T (B: P x Q), fused epilogue
@@ -162,7 +191,7 @@ nt_kernel(NtArgs a) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] = mfma4(st.bv[j][t], st.av[i][t], acc[i][j]);
+        for (int j = 0; j < TJ; ++j) mfma4_acc(acc[i][j], st.bv[j][t], st.av[i][t]);
   };
 
   // epilogue of row tile rt: lane holds row RT rt + 16i + c, columns cb + 16j + 4g .. +3;
@@ -264,6 +293,8 @@ nt_kernel(NtArgs a) {
       }
       mma(B);
     }
+    acc_fence();
+    acc_pin(acc);
     epilogue(rt);
   }
 }
@@ -367,6 +398,8 @@ dw_kernel(DwArgs a) {
     }
   }
 
+  acc_fence();
+  acc_pin(acc);
   // the four waves' tiles summed in LDS in wave order (deterministic), then one partial
   // tile per block; acc[i][j][r] is (n = nb + 4(4g + r) + i, k = kb + 4c + j)
   for (int w = 0; w < 4; ++w) {
@@ -429,9 +462,8 @@ __global__ void __launch_bounds__(256) dw_reduce_kernel(const float* __restrict_
 }
 
 // M in chunks whose A operands stay below 2^31 bytes (32-bit buffer offsets); a
-// persistent grid of 1,024 blocks walks each chunk's row tiles with 64 x 64 wave tiles
-// (two waves per SIMD). (128 x 128 wave tiles, 256 accumulators at one wave per SIMD,
-// were tried: the compiler spills 56-270 VGPRs for them.)
+// persistent grid walks each chunk's row tiles (64 x 64 wave tiles at two waves per SIMD,
+// 1,024 blocks; ANR_NERF_BIG=1: 128 x 128 at one wave per SIMD, 256 blocks, for P = 256)
 template <int WR, int WC, int TI, int TJ, int WPE>
 static void launch_cfg(const NtArgs& a, int64_t blocks_cap, hipStream_t st) {
   const int64_t rows = 16LL * TI * WR;
@@ -442,6 +474,11 @@ static void launch_cfg(const NtArgs& a, int64_t blocks_cap, hipStream_t st) {
   nt_kernel<WR, WC, TI, TJ, WPE><<<dim3(static_cast<unsigned>(gx), gy), 256, 0, st>>>(a);
 }
 
+// ANR_NERF_BIG=1: P = 256 layers on 128 x 128 wave tiles, 256 AGPR accumulators, one wave
+// per SIMD (the compiler spills 24 VGPRs of the epilogue's temporaries to scratch). The
+// kernels alone measured 3-6 % faster (profiles/r05_nerf_big_tiles.log), the NeRF step
+// the same (43.22 vs 43.17 ms), so the spill-free 64 x 64 form stays the default.
+static int g_nt_big = getenv("ANR_NERF_BIG") ? atoi(getenv("ANR_NERF_BIG")) : 0;
 static void launch_nt(NtArgs a, hipStream_t st) {
   const int64_t ld = a.lda1 > a.lda2 ? a.lda1 : a.lda2;
   const int64_t chunk = ((0x7fffffffLL / (ld * 4)) / 256) * 256;
@@ -455,6 +492,10 @@ static void launch_nt(NtArgs a, hipStream_t st) {
     b.c2 = a.c2 + r0 * a.ldc2;
     if (a.bits) b.bits = a.bits + r0 * a.wpr;
     if (a.mbits) b.mbits = a.mbits + r0 * a.wpr;
+    if (g_nt_big && a.P == 256) {
+      launch_cfg<2, 2, 8, 8, 1>(b, 256, st);
+      continue;
+    }
     if (a.P <= 128) {
       launch_cfg<2, 2, 4, 4, 2>(b, 1024, st);
       continue;

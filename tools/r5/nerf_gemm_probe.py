@@ -36,8 +36,10 @@ def main():
     st = _lib.stream(dev)
     lib = _lib.load()
     shapes = [(256, 256), (76, 256), (332, 256), (256, 260), (280, 128), (128, 4)]
-    if len(sys.argv) > 1:   # e.g. "256x256" (q x n): only that shape (counter passes)
-        shapes = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1:]]
+    args = [a for a in sys.argv[1:] if a != "--zeros"]
+    zeros = "--zeros" in sys.argv   # all-zero operands: the clock / data-toggling check
+    if args:   # e.g. "256x256" (q x n): only that shape (counter passes)
+        shapes = [tuple(int(v) for v in a.split("x")) for a in args]
     for (q, n) in shapes:
         x = torch.randn(M, q, device=dev)
         w = torch.randn(n, q, device=dev) * 0.05
@@ -53,6 +55,9 @@ def main():
         db = torch.zeros(n, device=dev)
         ws = torch.empty(lib.anr_nerf_linear_dw_workspace(M, n, q) // 4 + 4, device=dev)
         fl = 2.0 * M * n * q
+        if zeros:
+            for t in (x, w, b, g, wt):
+                t.zero_()
         bits = torch.empty(M, (n + 63) // 64, dtype=torch.int64, device=dev)
         mb = torch.full((M, (q + 63) // 64), 0x5555555555555555, dtype=torch.int64, device=dev)
         pq = q // 64 * 64   # the masked part of dX must be whole 64-column words

@@ -749,6 +749,11 @@ def main():
                     help="reference numerics: steps after the build-numerics warm start "
                          "before the --warmup / timed steps (the first --steps of them are "
                          "timed as transient_window); 0 = time right after the warm start")
+    ap.add_argument("--cold-start", action="store_true",
+                    help="reference numerics from the seed parameters: no build-numerics warm "
+                         "start, no settle (ADVICE r04: the number beside the warm-started "
+                         "headline; on the bench scene the field collapses, "
+                         "profiles/r05_*liveness*)")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every kernel timed (per-kernel breakdown)")
     args = ap.parse_args()
@@ -817,7 +822,8 @@ def main():
     pipe, bucket, opt = job.pipe, job.bucket, job.opt
     sharded = job.sharded
     step = job.step
-    warm = warm_start(job, args, cfg, ds, dev, rank, world, rank_batch, shard)
+    warm = (None if args.cold_start else
+            warm_start(job, args, cfg, ds, dev, rank, world, rank_batch, shard))
     transient = None
     if warm is not None and args.settle > 0:
         # The reference numerics' state right after the build-numerics warm start is a
@@ -1079,6 +1085,7 @@ def main():
             "dtype": args.dtype,
             "numerics": numerics,
             "warm_start": warm,
+            "start": "cold" if args.cold_start else ("warm" if warm else "seed"),
             "transient_window": transient,
             "d_enc_nonzero_frac": None if req is None else round(req[1], 4),
             "d_enc_nonzero_rows_frac": None if req is None else round(req[2], 4),

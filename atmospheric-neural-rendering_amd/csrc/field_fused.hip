@@ -1037,6 +1037,27 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     }
   }
+  // FAST full tiles hand their dL/denc rows to the NEXT tile's head, which stores them
+  // between its input conversion and its prefetch. Stored at the tile's end, they were the
+  // newest entries of the in-order vmcnt queue when the next head waited for its
+  // prefetched inputs, so every tile head also waited for the previous tile's store acks
+  // (vmcnt(0) a few instructions after the stores). The first head stores zeros to its own
+  // rows (rewritten by that tile's real values later, same wave, same addresses).
+  f4 pend[2][MT];
+  int64_t pend_tile = t_begin;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) pend[kt][mt] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto store_pend = [&]() {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int64_t row = pend_tile * TR + mt * 16 + li;
+        *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = pend[kt][mt];
+      }
+  };
   auto process = [&](auto full_c, int64_t tile, RawRows(&nraw)[MT], RawRows(&nnext)[MT]) {
     constexpr bool FULL = decltype(full_c)::value;
     {
@@ -1064,6 +1085,7 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         asm volatile("" : "+v"(rr.dc));
         raw_to_rows(rr, g, cur[mt]);
       }
+      store_pend();
       const int64_t tn = tile + 1 < t_full_end ? tile + 1 : tile;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) load_raw<ROWS>(a, tn * TR + mt * 16 + li, g, nnext[mt]);
@@ -1088,6 +1110,14 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       if (a.tile_nz && lane == 0) a.tile_nz[tile] = walk ? 1 : 0;
       if (!walk) {
         const f4 zero4 = {0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (FAST && FULL) {
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) pend[kt][mt] = zero4;
+          pend_tile = tile;
+          return;
+        }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int64_t row = tile * TR + mt * 16 + li;
@@ -1291,10 +1321,14 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
 #pragma unroll
               for (int i = 0; i < 4; ++i) v[i] = r16(r16(acc[mt][i]) * inv_s);
             }
-            *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
+            if constexpr (FAST && FULL)
+              pend[kt][mt] = v;
+            else
+              *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
           }
         }
       }
+      if constexpr (FAST && FULL) pend_tile = tile;
     }
     // the last dW MFMAs of the tile have written their accumulators before anything
     // (a loop-exit copy) reads them
@@ -1313,6 +1347,9 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       process(full_tile, tile + 1, nr1, nr0);
     }
     if (tile < t_full_end) process(full_tile, tile, nr0, nr1);
+    if constexpr (FAST) {
+      if (t_begin < t_full_end) store_pend();
+    }
   }
   for (int64_t tile = t_full_end > t_begin ? t_full_end : t_begin; tile < t_end; ++tile)
     process(std::integral_constant<bool, false>{}, tile, nr0, nr1);

@@ -114,7 +114,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
 nt_kernel(NtArgs a) {
   constexpr int RT = 16 * TI, CT = 16 * TJ;
   constexpr int NW = (CT + 63) / 64;  // bitmask words a wave tile's row spans
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the wave index through readfirstlane: the tile indices, the tile loop and its branches
+  // are then scalar (a per-lane `more` made the loads after it waterfall loops)
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int c = lane & 15, g = lane >> 4;
   // the bias, read by the epilogue, in LDS (zeros past P)
   __shared__ float sbias[16 * TJ * WC];
@@ -280,17 +283,21 @@ nt_kernel(NtArgs a) {
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = z4;
-    // invariant: A holds k-step s of this tile
+    // invariant: A holds k-step s of this tile. Every path issues the A loads, the last
+    // tile's final step included (it re-reads step 0 of its own tile, unused): the waitcnt
+    // pass merges the paths into the smallest outstanding count, so one path without them
+    // made mma(B) wait for the A loads just issued on every step (an exposed memory
+    // latency per k-step pair)
     for (int s = 0; s < nsteps; s += 2) {
       load(ocur, s + 1, B);
       if (s + 2 == nsteps) load_mask(rt);
       mma(A);
-      if (s + 2 < nsteps) {
-        load(ocur, s + 2, A);
-      } else if (more) {
-        offsets(rt + rts, ocur);
-        load(ocur, 0, A);
+      int sn = s + 2;
+      if (sn == nsteps) {
+        sn = 0;
+        if (more) offsets(rt + rts, ocur);
       }
+      load(ocur, sn, A);
       mma(B);
     }
     acc_fence();
@@ -324,7 +331,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 dw_kernel(DwArgs a) {
   __shared__ __attribute__((aligned(16))) float red[64 * 64];
   __shared__ float dbred[64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // a scalar wave index: the row range, and so every load's scalar offset, is then scalar
+  // (per lane, each buffer load compiled to a waterfall loop)
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int c = lane & 15, g = lane >> 4;
   const int nb = blockIdx.x * 64, kb = blockIdx.y * 64;
   const int s = blockIdx.z;
@@ -391,10 +401,18 @@ dw_kernel(DwArgs a) {
     load(m_begin, A);
     for (int st = 0; st < nst; st += 2) {
       const int64_t m0 = m_begin + 16LL * st;
+      // stage order pinned (sched_barrier): with scalar offsets the scheduler otherwise
+      // sinks each load to its first MFMA, where it waits for it
       load(m0 + 16, B);
+      __builtin_amdgcn_sched_barrier(0);
       mma(A);
-      if (st + 2 < nst) load(m0 + 32, A);
+      __builtin_amdgcn_sched_barrier(0);
+      // the last step's loads read past m_end (zeros, unused): with them every path issues
+      // the same loads, and mma(B) waits for B only (see nt_kernel)
+      load(m0 + 32, A);
+      __builtin_amdgcn_sched_barrier(0);
       mma(B);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 

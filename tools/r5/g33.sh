@@ -1,0 +1,20 @@
+#!/bin/bash
+# r5: field backward with the first-layer fragment preload (exp_libs/p0.so)
+# against the deferral-only library (exp_libs/defer.so): field kernel tests on the new library,
+# then alternating bench pairs (both numerics' dominant kernels in the `kernels` digest).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r5_g33; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py -k "field" > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
+tail -1 $O/test.log
+for rep in 1 2 3; do
+for v in p0 defer; do
+ANR_HIP_LIB=$PWD/exp_libs/$v.so timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-alt-numerics > $O/${v}_$rep.json.log 2>&1 || { tail -20 $O/${v}_$rep.json.log; exit 1; }
+python3 tools/r5/bench_line.py $O/${v}_$rep.json.log "$v rep $rep"
+done
+done
+for v in p0 defer; do
+ANR_HIP_LIB=$PWD/exp_libs/$v.so timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-alt-numerics --numerics build > $O/${v}_build.json.log 2>&1 || { tail -20 $O/${v}_build.json.log; exit 1; }
+python3 tools/r5/bench_line.py $O/${v}_build.json.log "$v build"
+done

@@ -109,7 +109,7 @@ constexpr uint32_t kOob = 0x80000000u;  // past every num_records: the load retu
 // holds there). Two operand stages alternate by unrolling the k loop by 2. The ReLU mask
 // of the input-gradient epilogue is one bit per element, written by the forward (32x less
 // than re-reading the f32 activations) and loaded a k-step before the tile ends.
-template <int WR, int WC, int TI, int TJ, int WPE>
+template <int WR, int WC, int TI, int TJ, int WPE, int NSTG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 nt_kernel(NtArgs a) {
   constexpr int RT = 16 * TI, CT = 16 * TJ;
@@ -165,7 +165,7 @@ nt_kernel(NtArgs a) {
     f4 av[TI], bv[TJ];
   };
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-  auto load = [&](const Offs& o, int s, Stage& st) {
+  auto load = [&](const Offs& o, int s, Stage& st, bool zero_partial = true) {
     const bool seg1 = s < s1steps;
     const int kl = seg1 ? 16 * s : 16 * (s - s1steps);
     const uint32_t sa = static_cast<uint32_t>(kl) * 4;
@@ -180,7 +180,7 @@ nt_kernel(NtArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < TJ; ++j) st.bv[j] = bload4(rbm, ob[j], sb);
-    if (kl + 16 > qs) {  // the segment's partial last k-step (wave-uniform branch)
+    if (zero_partial && kl + 16 > qs) {  // the segment's partial last k-step (uniform)
       const bool ok = kl + 4 * g < qs;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) st.bv[j] = ok ? st.bv[j] : z4;
@@ -275,6 +275,73 @@ nt_kernel(NtArgs a) {
 
   Offs ocur;
   offsets(rt0, ocur);
+  if constexpr (NSTG == 3) {
+    // Three operand stages, loads two k-steps ahead (the SQ counters of the two-stage
+    // loop still had its waves in s_waitcnt 27 % of their cycles: one k-step, 2 x 2,048
+    // MFMA cycles per SIMD, did not cover the operand latency). The k loop runs in steps
+    // of three; the padding steps (up to two) issue their loads but skip their MFMAs
+    // (wave-uniform branches around MFMAs only, so the load counts stay path-independent).
+    // Step indices past the tile's last are the next tile's (its row offsets, onext; the
+    // last tile re-reads its own, unused).
+    const int ns = s1steps + (a.q2 + 15) / 16;
+    const int nst = (ns + 2) / 3 * 3;
+    Offs onext;
+    auto ldx = [&](int j, Stage& st) {
+      const bool cur = j < nst;
+      Offs o;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        o.a1[i] = cur ? ocur.a1[i] : onext.a1[i];
+        o.a2[i] = cur ? ocur.a2[i] : onext.a2[i];
+      }
+      load(o, cur ? j : j - nst, st, false);
+    };
+    // k-step j of this tile: a padding step issues no MFMAs; a segment's partial last step
+    // zeroes B's lanes past the segment here, at its use (at load time that select waited
+    // for the loads just issued)
+    auto mmz = [&](int j, Stage& st) {
+      if (j >= ns) return;
+      const bool seg1 = j < s1steps;
+      const int kl = seg1 ? 16 * j : 16 * (j - s1steps);
+      const int qs = seg1 ? a.q1 : a.q2;
+      if (kl + 16 > qs) {
+        const bool ok = kl + 4 * g < qs;
+#pragma unroll
+        for (int jj = 0; jj < TJ; ++jj) st.bv[jj] = ok ? st.bv[jj] : z4;
+      }
+      mma(st);
+    };
+    Stage A, B, C;
+    load(ocur, 0, A, false);
+    load(ocur, 1, B, false);
+    for (int rt = rt0; rt < n_rt; rt += rts) {
+      const bool more = rt + rts < n_rt;
+      offsets(more ? rt + rts : rt, onext);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = z4;
+      // invariant: A holds k-step s, B step s + 1
+      for (int s = 0; s < nst; s += 3) {
+        ldx(s + 2, C);
+        if (s + 3 == nst) load_mask(rt);
+        mmz(s, A);
+        ldx(s + 3, A);
+        mmz(s + 1, B);
+        ldx(s + 4, B);
+        mmz(s + 2, C);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        ocur.a1[i] = onext.a1[i];
+        ocur.a2[i] = onext.a2[i];
+      }
+      acc_fence();
+      acc_pin(acc);
+      epilogue(rt);
+    }
+    return;
+  }
   Stage A, B;
   load(ocur, 0, A);
   for (int rt = rt0; rt < n_rt; rt += rts) {
@@ -482,6 +549,12 @@ __global__ void __launch_bounds__(256) dw_reduce_kernel(const float* __restrict_
 // M in chunks whose A operands stay below 2^31 bytes (32-bit buffer offsets); a
 // persistent grid walks each chunk's row tiles (64 x 64 wave tiles at two waves per SIMD,
 // 1,024 blocks; ANR_NERF_BIG=1: 128 x 128 at one wave per SIMD, 256 blocks, for P = 256)
+// Operand stages of the k loop: three (loads two k-steps ahead) unless ANR_NERF_STAGES=2
+// (A/B hook). Against two stages on one box: the NeRF step 41.5 -> 40.6 ms, the narrow
+// launches gaining most (256 x 260 forward 1.51 -> 1.40 ms: fc9's 4 density columns stream
+// A with little MFMA work per load); the 256 x 256 layers, which pay two padding steps per
+// tile, are unchanged (profiles/r05_nerf_stages_ab.log).
+static int g_nt_stages = getenv("ANR_NERF_STAGES") ? atoi(getenv("ANR_NERF_STAGES")) : 3;
 template <int WR, int WC, int TI, int TJ, int WPE>
 static void launch_cfg(const NtArgs& a, int64_t blocks_cap, hipStream_t st) {
   const int64_t rows = 16LL * TI * WR;
@@ -489,7 +562,11 @@ static void launch_cfg(const NtArgs& a, int64_t blocks_cap, hipStream_t st) {
   int64_t gx = ceil_div(a.M, rows);
   const int64_t cap = ceil_div(blocks_cap, gy);
   gx = gx < cap ? gx : cap;
-  nt_kernel<WR, WC, TI, TJ, WPE><<<dim3(static_cast<unsigned>(gx), gy), 256, 0, st>>>(a);
+  const dim3 grid(static_cast<unsigned>(gx), gy);
+  if (g_nt_stages != 2 && WPE == 2)
+    nt_kernel<WR, WC, TI, TJ, WPE, 3><<<grid, 256, 0, st>>>(a);
+  else
+    nt_kernel<WR, WC, TI, TJ, WPE, 2><<<grid, 256, 0, st>>>(a);
 }
 
 // ANR_NERF_BIG=1: P = 256 layers on 128 x 128 wave tiles, 256 AGPR accumulators, one wave

@@ -19,7 +19,10 @@ KERNELS = {"hash_fwd": "hashgrid_fwd_planes_kernel<",
            "field_bwd": "field::bwd_rt_kernel<64, 2, true, false",
            "sampler": "sample_uniform_bins_kernel",
            "comp_fwd": "ref16::fwd_kernel<",
-           "comp_bwd": "ref16::bwd_kernel<"}
+           "comp_bwd": "ref16::bwd_kernel<",
+           "nerf_nt_p256": "nerfmlp::nt_kernel<1, 4, 4, 4, 2>",
+           "nerf_nt_2x2": "nerfmlp::nt_kernel<2, 2, 4, 4, 2>",
+           "nerf_dw": "nerfmlp::dw_kernel("}
 
 
 def main(src):

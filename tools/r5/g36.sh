@@ -1,0 +1,11 @@
+#!/bin/bash
+# r5: SQ counter passes over the NeRF configs[1] step on the final library (after the
+# uniform-load fix), for the nt / dw kernels
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r5_g36; mkdir -p $O
+BENCH_ARGS="--workload nerf" bash tools/sq_bench.sh $O/sq > $O/sq.log 2>&1 || { tail -30 $O/sq.log; exit 1; }
+python3 tools/pmc_table.py $O/sq > $O/sq_table.txt
+rm -rf $O/sq/p1 $O/sq/p2 $O/sq/p3
+awk '/== nerf/,0' $O/sq_table.txt

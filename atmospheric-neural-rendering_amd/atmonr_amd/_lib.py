@@ -299,11 +299,6 @@ _SIGNATURES = {
         [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
          c_int64, _P, c_int64, _P, _P, c_float, _P],
     ),
-    "anr_ingp_field_bwd_ref16_h": (
-        c_int32,
-        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
-         c_int64, _P, c_int64, _P, _P, c_float, _P],
-    ),
     "anr_ingp_field_bwd_ref16_tiles": (
         c_int32,
         [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,

@@ -182,14 +182,10 @@ class IngpFieldFn(torch.autograd.Function):
             d_color = torch.zeros(M, pipe.dir_mlp.n_output_dims, device=dev)
         d_color = d_color.float().contiguous()
         d_sigma = d_sigma.float().contiguous() if d_sigma is not None else None
+        d_enc = torch.empty(M, pipe.pos_encoder.hash_grids[0].n_out, device=dev, dtype=torch.float32)
         pdesc, ddesc = ctypes.byref(pipe.pos_mlp.desc), ctypes.byref(pipe.dir_mlp.desc)
         mma = _mma_code(pipe)
         ls = getattr(pipe, "loss_scale", None)
-        # reference numerics, ANR_DENC_F16=1: dL/denc travels as f16 (exact; not with the
-        # tile path)
-        half = bool(ls) and _DENC_F16 and not _TILE_SKIP
-        d_enc = torch.empty(M, pipe.pos_encoder.hash_grids[0].n_out, device=dev,
-                            dtype=torch.float16 if half else torch.float32)
         tiles = None
         if ls:
             # reference numerics: tcnn's loss-scaled f16 backward. ANR_TILE_SKIP=1: it also
@@ -205,8 +201,7 @@ class IngpFieldFn(torch.autograd.Function):
                      d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
                      float(ls), ptr(tiles), s, tag="field_bwd")
             else:
-                call("anr_ingp_field_bwd_ref16_h" if half else "anr_ingp_field_bwd_ref16",
-                     pdesc, ddesc, ptr(packed), ptr(enc),
+                call("anr_ingp_field_bwd_ref16", pdesc, ddesc, ptr(packed), ptr(enc),
                      ctx.enc_ld, ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
                      d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
                      float(ls), s, tag="field_bwd")
@@ -236,8 +231,7 @@ class IngpFieldFn(torch.autograd.Function):
                  tag="hash_bwd")
         else:
             call("anr_hashgrid_bwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(d_enc),
-                 _lib.F16 if half else _lib.F32, d_enc.stride(0), ptr(g_hash), s,
-                 tag="hash_bwd")
+                 _lib.F32, d_enc.stride(0), ptr(g_hash), s, tag="hash_bwd")
         _done(direct_h, p_hash)
         return (None, None, None, None if direct_h else g_hash, None if direct_p else g_pos,
                 None if direct_d else g_dir, None, None, None)
@@ -256,11 +250,6 @@ def _enc_planes(grid) -> bool:
 
 _ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"
 _TILE_SKIP = os.environ.get("ANR_TILE_SKIP", "0") != "0"
-# reference numerics: ANR_DENC_F16=1 passes dL/denc between the field and hash-grid
-# backwards as f16 (exact: its values are f16 values; half the bytes). Off by default:
-# measured no faster (2.707 / 2.727 / 2.772 vs 2.717 / 2.733 / 2.727 ms per step, hash bwd
-# unchanged: it is bound by its walk, not by reading dL/denc; profiles/r05_denc_f16_ab.log)
-_DENC_F16 = os.environ.get("ANR_DENC_F16", "0") != "0"
 
 
 def field_fused(pipe) -> bool:

@@ -279,11 +279,6 @@ struct Args {
   // tile was walked), 0 if it was skipped (dL/denc rows zero) -- the hash-grid backward
   // then skips those rows without loading them (anr_hashgrid_bwd_tiles)
   uint8_t* tile_nz;
-  // nullable, reference numerics only: dL/denc written as f16 here instead of f32 to d_enc
-  // (same row stride in elements). The reference numerics' dL/denc values are f16 values
-  // (f16(f16(g) / 128)), so the f16 copy is exact at half the bytes for the field backward
-  // to write and the hash-grid backward to read.
-  _Float16* d_enc_h;
 };
 
 // ROWS is a compile-time choice: a run-time test on a.rows in the prefetch paths put a
@@ -1054,23 +1049,14 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) pend[kt][mt] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-  // one lane's 4 dL/denc values of row `row`, columns 16 kt + 4 g .. + 3 (f32, or f16 into
-  // d_enc_h under the reference numerics: one store instruction either way)
-  auto store_enc = [&](int64_t row, int kt, const f4& v) {
-    if constexpr (REF) {
-      if (a.d_enc_h) {
-        *reinterpret_cast<h4*>(a.d_enc_h + row * a.d_enc_stride + 16 * kt + 4 * g) =
-            __builtin_convertvector(v, h4);
-        return;
-      }
-    }
-    *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
-  };
   auto store_pend = [&]() {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) store_enc(pend_tile * TR + mt * 16 + li, kt, pend[kt][mt]);
+      for (int mt = 0; mt < MT; ++mt) {
+        const int64_t row = pend_tile * TR + mt * 16 + li;
+        *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = pend[kt][mt];
+      }
   };
   auto process = [&](auto full_c, int64_t tile, RawRows(&nraw)[MT], RawRows(&nnext)[MT]) {
     constexpr bool FULL = decltype(full_c)::value;
@@ -1137,7 +1123,8 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
           const int64_t row = tile * TR + mt * 16 + li;
           if (full || row < a.M) {
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt) store_enc(row, kt, zero4);
+            for (int kt = 0; kt < 2; ++kt)
+              *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = zero4;
           }
         }
         return;
@@ -1337,7 +1324,7 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
             if constexpr (FAST && FULL)
               pend[kt][mt] = v;
             else
-              store_enc(row, kt, v);
+              *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
           }
         }
       }
@@ -1705,7 +1692,7 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
                      const float* d_color, int64_t d_color_stride, float* d_enc,
                      int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
                      int64_t workspace_bytes, anr_stream_t stream, float loss_scale = 0.0f,
-                     uint8_t* tile_nz = nullptr, _Float16* d_enc_h = nullptr) {
+                     uint8_t* tile_nz = nullptr) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_bwd: unsupported pos/dir MLP pair");
   ANR_CHECK_ARG(loss_scale == 0.0f || (loss_scale > 0.0f && mma_dtype == ANR_F16 && rows == nullptr),
@@ -1713,15 +1700,14 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   ANR_CHECK_ARG(mma_ok(mma_dtype), "anr_ingp_field_bwd: mma_dtype must be ANR_F16 or ANR_BF16");
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_bwd: bad M");
   if (M == 0) return ANR_OK;
-  ANR_CHECK_ARG(packed && enc && dirs && d_color && (d_enc || d_enc_h) && g_pos && g_dir,
+  ANR_CHECK_ARG(packed && enc && dirs && d_color && d_enc && g_pos && g_dir,
                 "anr_ingp_field_bwd: null pointer");
   ANR_CHECK_ARG(n_per_ray >= 1 && n_per_ray < (1LL << 31) && d_color_stride >= dir->n_output &&
                     d_enc_stride >= 32 && d_enc_stride % 4 == 0,
                 "anr_ingp_field_bwd: bad shape/stride");
   ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(enc) & 15) == 0 &&
                     (reinterpret_cast<uintptr_t>(packed) & 15) == 0 &&
-                    (reinterpret_cast<uintptr_t>(d_enc) & 15) == 0 &&
-                    (reinterpret_cast<uintptr_t>(d_enc_h) & 15) == 0,
+                    (reinterpret_cast<uintptr_t>(d_enc) & 15) == 0,
                 "anr_ingp_field_bwd: enc/packed/d_enc must be 16-byte aligned");
   Args a{};
   a.packed = static_cast<const _Float16*>(packed);
@@ -1742,7 +1728,6 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   a.rows = rows;
   a.loss_scale = loss_scale;
   a.tile_nz = tile_nz;
-  a.d_enc_h = d_enc_h;
   const int rc = dispatch(v, mma_dtype == ANR_BF16, 2, a, static_cast<float*>(workspace),
                           workspace_bytes, reinterpret_cast<hipStream_t>(stream));
   ANR_CHECK_ARG(rc != 2,
@@ -1811,20 +1796,6 @@ extern "C" int anr_ingp_field_bwd_ref16(const anr_mlp_desc* pos, const anr_mlp_d
   return field_bwd(pos, dir, ANR_F16, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
                    d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, nullptr,
                    0, stream, loss_scale);
-}
-
-extern "C" int anr_ingp_field_bwd_ref16_h(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                                          const void* packed, const void* enc,
-                                          int64_t enc_stride, const float* dirs,
-                                          int64_t n_per_ray, int64_t M, const float* d_sigma,
-                                          const float* d_color, int64_t d_color_stride,
-                                          void* d_enc, int64_t d_enc_stride, float* g_pos,
-                                          float* g_dir, float loss_scale, anr_stream_t stream) {
-  ANR_CHECK_ARG(loss_scale > 0.0f, "anr_ingp_field_bwd_ref16_h: loss_scale must be > 0");
-  ANR_CHECK_ARG(d_enc != nullptr, "anr_ingp_field_bwd_ref16_h: null d_enc");
-  return field_bwd(pos, dir, ANR_F16, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
-                   d_sigma, d_color, d_color_stride, nullptr, d_enc_stride, g_pos, g_dir,
-                   nullptr, 0, stream, loss_scale, nullptr, static_cast<_Float16*>(d_enc));
 }
 
 extern "C" int anr_ingp_field_bwd_ref16_tiles(const anr_mlp_desc* pos, const anr_mlp_desc* dir,

@@ -565,18 +565,6 @@ int anr_ingp_field_bwd_ref16(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
                              int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
                              float* g_pos, float* g_dir, float loss_scale,
                              anr_stream_t stream);
-/* anr_ingp_field_bwd_ref16 writing dL/denc as f16 (d_enc: M rows of d_enc_stride f16,
- * 16-byte aligned) instead of f32. Exact: the reference numerics' dL/denc values are f16
- * values (tinycudann/modules.py casts input_grad / loss_scale to the f16 input's dtype);
- * half the bytes for this kernel to write and anr_hashgrid_bwd (dout_dtype ANR_F16) to
- * read. Replaces the same call site as anr_ingp_field_bwd_ref16. */
-int anr_ingp_field_bwd_ref16_h(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
-                               const void* packed, const void* enc, int64_t enc_stride,
-                               const float* dirs, int64_t n_per_ray, int64_t M,
-                               const float* d_sigma, const float* d_color,
-                               int64_t d_color_stride, void* d_enc, int64_t d_enc_stride,
-                               float* g_pos, float* g_dir, float loss_scale,
-                               anr_stream_t stream);
 /* anr_ingp_field_bwd_ref16 that also writes, per 32-row tile t of the M rows, tile_nz[t]
  * = 1 if any row of the tile had a nonzero dL/dcolor or dL/dsigma (the tile was walked)
  * and 0 otherwise (skipped: its dL/denc rows are written as 0). tile_nz: ceil(M / 32)

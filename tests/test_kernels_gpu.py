@@ -1320,57 +1320,3 @@ def test_hashgrid_bwd_tiles_equals_plain(dev, M):
     assert torch.isfinite(gb).all()
     assert (ga - gb).abs().max().item() <= 1e-5 * ga.abs().max().item()
     assert ((ga != 0) == (gb != 0)).float().mean().item() > 0.9999
-
-
-@pytest.mark.parametrize("n_per_ray,R,extra", [(1024, 5, 0), (64, 9, 13)])
-def test_ingp_field_bwd_ref16_f16_out_exact(dev, n_per_ray, R, extra):
-    """anr_ingp_field_bwd_ref16_h writes the reference numerics' dL/denc as f16: the same
-    values as anr_ingp_field_bwd_ref16's f32 output (they are f16 values), bit for bit, the
-    same parameter gradients up to the flush order, and the hash-grid backward reading the
-    f16 copy gives the table gradient of the f32 one (same sums, f32 atomic order)."""
-    from atmonr_amd import _lib
-
-    width, nhd, nb = 64, 2, 4
-    M = R * n_per_ray + extra
-    g = torch.Generator(device=dev).manual_seed(31)
-    lib = _lib.load()
-    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
-    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
-    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
-    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
-    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
-    dirs = torch.rand(R + 1, 3, device=dev, generator=g)
-    s = _lib.stream(dev)
-    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
-    _lib.call("anr_ingp_field_pack", pb, db, _lib.F16, pp.data_ptr(), pd.data_ptr(),
-              packed.data_ptr(), s)
-    dcol = (torch.randn(M, nb, device=dev, generator=g) * 1e-2).half().float()
-    dsig = (torch.randn(M, device=dev, generator=g) * 1e-3).half().float()
-    dcol[: M // 3] = 0.0  # all-zero tiles (the skip path's stores) as well
-    dsig[: M // 3] = 0.0
-    outs = {}
-    for name, dt in (("f32", torch.float32), ("f16", torch.float16)):
-        d_enc = torch.full((M, 32), 7.0, device=dev, dtype=dt)
-        g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
-        fn = "anr_ingp_field_bwd_ref16_h" if dt == torch.float16 else "anr_ingp_field_bwd_ref16"
-        _lib.call(fn, pb, db, packed.data_ptr(), enc.data_ptr(), 32, dirs.data_ptr(),
-                  n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb, d_enc.data_ptr(), 32,
-                  g_pos.data_ptr(), g_dir.data_ptr(), 128.0, s)
-        outs[name] = (d_enc, g_pos, g_dir)
-    torch.cuda.synchronize()
-    a, b = outs["f32"], outs["f16"]
-    assert torch.equal(a[0].half(), b[0]) and torch.equal(a[0], b[0].float())
-    assert (a[0][: M // 3] == 0).all()
-    for x, y in zip(a[1:], b[1:]):
-        assert (x - y).abs().max().item() <= 2e-5 * y.abs().max().item()
-    # the hash-grid backward from either copy
-    d = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, 19)
-    x = torch.rand(M, 3, device=dev, generator=g)
-    ga, gb = torch.zeros(d.n_params, device=dev), torch.zeros(d.n_params, device=dev)
-    _lib.call("anr_hashgrid_bwd", ctypes.byref(d), x.data_ptr(), 3, M, a[0].data_ptr(),
-              _lib.F32, 32, ga.data_ptr(), s)
-    _lib.call("anr_hashgrid_bwd", ctypes.byref(d), x.data_ptr(), 3, M, b[0].data_ptr(),
-              _lib.F16, 32, gb.data_ptr(), s)
-    torch.cuda.synchronize()
-    assert (ga - gb).abs().max().item() <= 1e-5 * ga.abs().max().item()
-    assert torch.equal(ga != 0, gb != 0)

@@ -24,7 +24,11 @@
 
 // Profiling ablation (tools): 1 = backward without its atomics. 0 in product builds.
 #ifndef HASH_BS
-#define HASH_BS 8  // samples per prefetch batch of the v2 backward walker
+// samples per prefetch batch of the v2 backward walker. 6 rather than 8: the batch's
+// scalar coordinates (two batches of 3 x BS SGPRs) spilled 40 SGPRs at 8, 3 at 6; on the
+// settled reference-numerics step's own inputs 0.717 -> 0.690 ms (with the max-ILP
+// scheduler 0.689; profiles/r05_hash_bwd_variants.log). The tile path keeps 8.
+#define HASH_BS 6
 #endif
 #ifndef HASH_FBS
 #define HASH_FBS 4  // samples per coordinate prefetch batch of the forward walker
@@ -792,7 +796,7 @@ __device__ __forceinline__ uint32_t distinct_segments(bool active, uint64_t seg)
 // COUNT: the request-count instrument (anr_hashgrid_bwd_count_requests): the same walk,
 // but every flush instruction adds its number of distinct 64-B segments to *count
 // instead of issuing the atomics (dtable is not written)
-template <int D, typename TG, int XS, int DS, bool COUNT = false>
+template <int D, typename TG, int XS, int DS, bool COUNT = false, int BSZ = HASH_BS>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride_rt, int64_t M,
     int64_t K, const TG* __restrict__ dout, int64_t dout_stride_rt, float* __restrict__ dtable,
@@ -893,7 +897,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
 
   // Batches of BS samples: the next batch's coordinates and gradients are loaded while
   // this one is processed (indices clamped to the chunk, so the loads need no branch).
-  constexpr int BS = HASH_BS;
+  constexpr int BS = BSZ;
   float xb[BS][D], xn[BS][D];
   TG gb[BS], gn[BS];
   const int col = level * 2 + f;
@@ -968,7 +972,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
       for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
     }
   };
-  if (tile_nz == nullptr) {
+  if (BSZ != 8 || tile_nz == nullptr) {  // the tile mask below is laid out for BS = 8
     load_batch(m0, xb, gb);
     for (int64_t mb = m0; mb < m1; mb += BS) {
       load_batch(mb + BS, xn, gn);
@@ -1433,12 +1437,12 @@ extern "C" int anr_hashgrid_bwd_tiles(const anr_hashgrid_desc* d, const float* x
   }
   const dim3 grid(static_cast<unsigned>(ceil_div(ceil_div(M, K), 4))), block(256);
   if (dout_dtype == ANR_F16)
-    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, __half, 3, 32>), grid, block, 0,
+    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, __half, 3, 32, false, 8>), grid, block, 0,
                        as_stream(stream), G, d->n_levels, x, x_stride, M, K,
                        static_cast<const __half*>(dout), dout_stride, dtable, bwd_skip_zero(),
                        nullptr, tile_nz);
   else
-    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, float, 3, 32>), grid, block, 0,
+    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, float, 3, 32, false, 8>), grid, block, 0,
                        as_stream(stream), G, d->n_levels, x, x_stride, M, K,
                        static_cast<const float*>(dout), dout_stride, dtable, bwd_skip_zero(),
                        nullptr, tile_nz);

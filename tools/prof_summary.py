@@ -40,7 +40,7 @@ def source_sha1(tag: str) -> str | None:
 TAGS = {  # prefixes: one instantiation of each per bench run (width / dtype follow --variant, --dtype)
     "hash_fwd": "hashgrid_fwd_v6_kernel<3,",
     "hash_fwd_v1": "hashgrid_fwd_kernel<3,",
-    "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32, false>",
+    "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32, false, 6>",
     "hash_bwd_rtstride": "hashgrid_bwd_v2_kernel<3, float, 0, 0>",
     "field_fwd": "field::fwd_kernel<",
     "field_bwd": "field::bwd_rt_kernel<",

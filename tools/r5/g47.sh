@@ -1,0 +1,19 @@
+#!/bin/bash
+# r5: hash-grid backward at batch 6 + max-ILP (in-tree library = exp_libs/new.so) against the
+# previous library (exp_libs/cur.so): hash-grid tests, then alternating bench lines
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r5_g47; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py -k "hashgrid or field" > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
+tail -1 $O/test.log
+for rep in 1 2; do
+for v in new cur; do
+ANR_HIP_LIB=$PWD/exp_libs/$v.so timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-alt-numerics > $O/${v}_$rep.json.log 2>&1 || { tail -20 $O/${v}_$rep.json.log; exit 1; }
+python3 tools/r5/bench_line.py $O/${v}_$rep.json.log "$v rep $rep"
+done
+done
+for v in new cur; do
+ANR_HIP_LIB=$PWD/exp_libs/$v.so timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-alt-numerics --numerics build > $O/${v}_build.json.log 2>&1 || { tail -20 $O/${v}_build.json.log; exit 1; }
+python3 tools/r5/bench_line.py $O/${v}_build.json.log "$v build"
+done

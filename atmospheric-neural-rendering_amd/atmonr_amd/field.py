@@ -67,7 +67,7 @@ class IngpFieldFn(torch.autograd.Function):
         dirs = dirs.float().contiguous()
 
         fused = field_fused(pipe) and enc_mod.dtype == torch.float16
-        if fused and _enc_planes(grid):
+        if fused and _enc_planes(grid, M):
             # level-quad planes (anr_hashgrid_fwd_planes: one lane per sample, coalesced;
             # 0.47-0.50 ms vs the row-layout walker's 0.63 at the bench shape), handed to the
             # field kernels as enc_stride = -plane
@@ -241,11 +241,15 @@ def _mma_code(pipe) -> int:
     return _lib.BF16 if pipe.pos_mlp.dtype == torch.bfloat16 else _lib.F16
 
 
-def _enc_planes(grid) -> bool:
+def _enc_planes(grid, M: int) -> bool:
     """The fused field reads the hash features as level-quad planes (default) or, with
-    ANR_ENC_PLANES=0 (A/B), in the row layout of the walker forward."""
+    ANR_ENC_PLANES=0 (A/B), in the row layout of the walker forward. The planes kernel
+    addresses its output with 32-bit byte offsets (16 B per sample and quad): above ~33 M
+    samples at 16 levels the row layout (whose walker falls back to 64-bit indexing) runs."""
     d = grid.desc
-    return (_ENC_PLANES and d.n_features == 2 and d.n_levels <= 16 and d.n_dims == 3)
+    nq = (d.n_levels + 3) // 4
+    return (_ENC_PLANES and d.n_features == 2 and d.n_levels <= 16 and d.n_dims == 3
+            and 16 * nq * (M + 256) < 2 ** 31)
 
 
 _ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"

@@ -47,6 +47,17 @@ def _native_ok(x: torch.Tensor) -> bool:
             and x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
 
 
+def _native_net_ok(net: "AtmoNeRF", x: torch.Tensor, with_dir: bool) -> bool:
+    """The shapes csrc/nerf_mlp.hip's entry points accept (hidden width a multiple of 64,
+    4-aligned channel segments) and a dense f32 input; otherwise the library path runs."""
+    if not (_native_ok(x) and net.hidden_dim % 64 == 0 and net.pos_channels % 4 == 0):
+        return False
+    if with_dir:
+        return (net.dir_channels % 4 == 0
+                and x.shape[1] == net.pos_channels + net.dir_channels)
+    return x.shape[1] == net.pos_channels
+
+
 def _wt(layer: nn.Linear) -> tuple[torch.Tensor, int]:
     """(W^T as (in, round_up(out, 4)) with zero pad columns, its row stride)."""
     w = layer.weight.detach()
@@ -322,7 +333,7 @@ class AtmoNeRF(nn.Module):
 
     def forward_pos_only(self, x_pos: torch.Tensor, noise: torch.Tensor | None = None):
         """models/nerf.py:48-71: returns (fc9 output, relu(sigma [+ noise if training]))."""
-        if not torch.is_grad_enabled() and _native_ok(x_pos):
+        if not torch.is_grad_enabled() and _native_net_ok(self, x_pos, with_dir=False):
             y9 = _mlp_forward(self, x_pos, pos_only=True)[8]
             x = y9[:, : self.fc9.out_features]
             sigma = x[:, self.hidden_dim:]
@@ -349,9 +360,7 @@ class AtmoNeRF(nn.Module):
     def forward(self, x: torch.Tensor, noise: torch.Tensor | None = None):
         """models/nerf.py:73-93: (sigmoid color, sigma). fc9's hidden part feeds fc10
         without an activation, as in the reference."""
-        if (_native_ok(x) and x.shape[1] == self.pos_channels + self.dir_channels
-                and self.hidden_dim % 64 == 0 and self.pos_channels % 4 == 0
-                and self.dir_channels % 4 == 0):
+        if _native_net_ok(self, x, with_dir=True):
             if self.training and noise is None:
                 noise = torch.randn(x.shape[0], self.volume_channels, device=x.device)
             return _AtmoNeRFFn.apply(x, noise if self.training else None, self,

@@ -168,7 +168,8 @@ class FusedAdam(torch.optim.Optimizer):
         mode with device state built, the loaded values are copied INTO the existing
         exp_avg / exp_avg_sq / device step / lr storage instead, so a captured step
         (GraphedTrainStep) keeps pointing at live memory and replays from the loaded state.
-        When that is impossible (new parameters, shapes, mixed steps) the device state is
+        When that is impossible (new parameters, shapes, mixed steps, a different weight
+        decay, which the captured launch holds by value) the device state is
         dropped and ``generation`` bumped: a graph built on it recaptures before replaying."""
         if not (self.capturable and self._devstate):
             super().load_state_dict(state_dict)
@@ -201,8 +202,15 @@ class FusedAdam(torch.optim.Optimizer):
                 if len(steps) != 1:
                     ok = False
                     break
+                new_groups = [group_of[id(p)] for p in ds["params"]]
+                # weight decay is captured by value in the launch descriptors: a loaded
+                # value that differs needs a recapture, not an in-place reload
+                if ([float(g["weight_decay"]) for g in ds["groups"]]
+                        != [float(g["weight_decay"]) for g in new_groups]):
+                    ok = False
+                    break
                 ds["step"].fill_(steps.pop())
-                ds["groups"] = [group_of[id(p)] for p in ds["params"]]
+                ds["groups"] = new_groups
                 ds["lr_host"] = None  # sync_hyper rewrites the lr tensor in place
         if ok:
             # same parameters in the same launch order; only the group dicts are new

@@ -234,19 +234,21 @@ class ShardedAdam(torch.optim.Optimizer):
     one all-to-all and sums the W received slices in f32 on the owner -- 2n + 2n bytes,
     exact when every gradient value is an f16 number, as under the reference numerics
     (tinycudann's f16 parameter gradients, quantised per rank before the exchange); a
-    gradient that is not f16-exact is refused (``check_f16``, on the first step). Parameters become views into one flat f32 buffer (padded to a
+    gradient that is not f16-exact is refused (``check_f16``: on the first step and every
+    ``check_every`` steps). Parameters become views into one flat f32 buffer (padded to a
     multiple of W). ``update(segments, step, betas, eps, decoupled)`` applies the update
     (default: the HIP multi-tensor kernel; tests inject a reference)."""
 
     def __init__(self, bucket: FlatGradBucket, param_groups: list, betas=(0.9, 0.999),
                  eps: float = 1e-8, decoupled: bool = True, gather: str = "f16", group=None,
                  update=hip_adam_update, lr: float = 1e-3, weight_decay: float | None = None,
-                 exchange: str = "f32", check_f16: bool = True):
+                 exchange: str = "f32", check_f16: bool = True, check_every: int = 256):
         if gather not in ("f16", "f32"):
             raise ValueError("gather: 'f16' or 'f32'")
         if exchange not in ("f16", "f32"):
             raise ValueError("exchange: 'f16' or 'f32'")
         self.exchange, self.check_f16 = exchange, check_f16
+        self.check_every = max(1, int(check_every))
         if weight_decay is None:  # FusedAdam's default: torch.optim.AdamW's 1e-2, Adam's 0
             weight_decay = 1e-2 if decoupled else 0.0
         super().__init__(param_groups, dict(lr=lr, betas=tuple(betas), eps=eps,
@@ -312,11 +314,17 @@ class ShardedAdam(torch.optim.Optimizer):
         lo = self.rank * self.S
         if self.world > 1 and self.exchange == "f16":
             half = self.bucket.flat.to(torch.float16)
-            # checked on the first step (a guard against pairing it with f32 gradients)
-            if self.check_f16 and self.steps == 0 and not torch.equal(half.float(),
-                                                                      self.bucket.flat):
-                raise ValueError("ShardedAdam(exchange='f16'): the gradient holds values that "
-                                 "are not f16 numbers (quantise them first, or exchange in f32)")
+            # checked on the first step and every check_every steps after it (a guard
+            # against pairing it with f32 gradients, e.g. a module added to the bucket
+            # without the end-of-backward quantisation); NaN entries are not compared (a
+            # non-finite gradient is the loss scaler's business, not a layout error)
+            if self.check_f16 and self.steps % self.check_every == 0:
+                flat = self.bucket.flat
+                same = (half.float() == flat) | torch.isnan(flat)
+                if not bool(same.all()):
+                    raise ValueError(
+                        "ShardedAdam(exchange='f16'): the gradient holds values that are not "
+                        "f16 numbers (quantise them first, or exchange in f32)")
             recv = torch.empty_like(half)
             # slice r of every rank's gradient lands on rank r: recv[j * S:(j + 1) * S] is
             # rank j's contribution, summed here in f32 in rank order

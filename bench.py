@@ -20,11 +20,18 @@ would time a dead field); the build numerics are timed in the same run (``alt_nu
 per batch, forward only) in points/s.
 
 ``--workload nerf`` measures BASELINE configs[1] instead (configs/nerf.json, batch 4096,
-f32 library GEMMs; see run_nerf). Rank 0 prints ONE JSON line. ``roofline`` is for the kernel that takes the most time per
-step, timed with HIP events on the launch stream inside the timed region; its
-algorithmic bytes / FLOPs per launch (kernel_models) are compulsory
-HBM traffic and dense MFMA work, and the bound is whichever fraction of peak is larger. ``cpu_baseline`` times the
-oracle's CPU restatement of the configs/nerf.json train step (rank 0, N = 1 only).
+native f32 MFMA layers; see run_nerf). Rank 0 prints ONE JSON line.
+
+``roofline`` is for the kernel that takes the most time per step, timed with HIP events on
+the launch stream inside the timed region; its algorithmic bytes / FLOPs per launch
+(kernel_models) are compulsory HBM traffic and dense MFMA work (the field
+backward: dX + dW, the recomputed forward reported beside). ``peak`` / ``frac`` are against
+the spec sheet (MI355X_MICROARCH.md: 8 TB/s, 2.5 PF/s f16); ``measured_ceiling`` gives the
+fraction of the ceilings tools/ubench measures on the box in the same run. The bound is
+whichever spec fraction is larger. ``roofline_targets`` lists north_star's two kernel
+targets (hash encode >= 0.70 of HBM, fused MLP >= 0.50 of MFMA) for all four kernels.
+``cpu_baseline`` times the oracle's CPU restatement of the configs/nerf.json train step
+(rank 0, N = 1 only) on every core of the process's affinity mask.
 """
 
 from __future__ import annotations
@@ -109,8 +116,10 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
         "field_fwd": {"bytes": M * (enc_b + 4 + 4 * nb), "flops": M * f_fwd},
         # enc in, sigma out; the pos MLP only (extract / occupancy)
         "field_density": {"bytes": M * (enc_b + 4), "flops": M * mlp_flops(pos)},
-        # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; forward recompute + dX + dW
-        "field_bwd": {"bytes": M * (enc_b + 4 * nb + 4 + 4 * grid.n_out), "flops": 3 * M * f_fwd},
+        # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; dX + dW (2x the forward) is the
+        # algorithmic work, the forward the kernel recomputes is reported beside it
+        "field_bwd": {"bytes": M * (enc_b + 4 * nb + 4 + 4 * grid.n_out), "flops": 2 * M * f_fwd,
+                      "flops_with_recompute": 3 * M * f_fwd},
     }
     ent, stale = pmc_entry(pmc, "hash_bwd", key_sfx)
     if requests is not None:
@@ -189,24 +198,61 @@ def count_hash_requests(job, n_samples: int) -> tuple[int, float, float] | None:
 
 
 def _roof(mdl: dict, avg_ms: float, peaks: dict, mfma_key: str) -> dict:
+    """Achieved rates of one kernel and their fractions of peak. The ``*_frac`` fields are
+    against the spec sheet (MI355X_MICROARCH.md: HBM3E 8 TB/s, dense f16/bf16 MFMA
+    2.5 PF/s, the 'Global float atomics' 64-B request rate); ``*_frac_measured`` against
+    the ceilings tools/ubench measured on this box in the same run. The bound is the
+    larger spec fraction. ``flops`` is algorithmic work (for the field backward dX + dW,
+    2x the forward); ``flops_with_recompute`` adds the forward the kernel recomputes."""
     sec = avg_ms * 1e-3
     gbs = mdl["bytes"] / sec / 1e9
     tfs = mdl["flops"] / sec / 1e12
-    fb, ff = gbs / peaks["hbm_copy_gbs"], tfs / peaks[mfma_key]
+    fb, ff = gbs / SPEC_PEAKS["hbm_copy_gbs"], tfs / SPEC_PEAKS[mfma_key]
     r = {"hbm_gbs": round(gbs, 1), "hbm_frac": round(fb, 4), "mfma_tfs": round(tfs, 2),
-         "mfma_frac": round(ff, 4), "bound": "hbm" if fb >= ff else "mfma"}
+         "mfma_frac": round(ff, 4),
+         "hbm_frac_measured": round(gbs / peaks["hbm_copy_gbs"], 4),
+         "mfma_frac_measured": round(tfs / peaks[mfma_key], 4),
+         "bound": "hbm" if fb >= ff else "mfma"}
+    if mdl.get("flops_with_recompute"):
+        tr = mdl["flops_with_recompute"] / sec / 1e12
+        r["mfma_tfs_with_recompute"] = round(tr, 2)
+        r["mfma_frac_with_recompute"] = round(tr / SPEC_PEAKS[mfma_key], 4)
+        r["mfma_frac_with_recompute_measured"] = round(tr / peaks[mfma_key], 4)
     if "survey_bytes" in mdl:
         sg = mdl["survey_bytes"] / sec / 1e9
         r["survey_model_gbs"] = round(sg, 1)
-        r["survey_model_frac"] = round(sg / peaks["hbm_copy_gbs"], 4)
+        r["survey_model_frac"] = round(sg / SPEC_PEAKS["hbm_copy_gbs"], 4)
     if "atomic_requests" in mdl:
         rq = mdl["atomic_requests"] / sec / 1e9
-        fa = rq / peaks["atomic_seg16_greq_s"]
+        fa = rq / SPEC_PEAKS["atomic_seg16_greq_s"]
         r["atomic_greq_s"] = round(rq, 3)
         r["atomic_frac"] = round(fa, 4)
+        r["atomic_frac_measured"] = round(rq / peaks["atomic_seg16_greq_s"], 4)
         if fa >= max(fb, ff):
             r["bound"] = "atomic"
     return r
+
+
+def target_rooflines(kernels: dict, mfma_key: str) -> dict:
+    """north_star's two kernel targets from the per-kernel table, against the spec peaks:
+    the hash-encode kernels' compulsory-byte HBM fraction (target >= 0.70) and the fused
+    MLP kernels' MFMA fraction (target >= 0.50)."""
+    out = {}
+    for name, key, tgt in (("hash_fwd", "hbm_frac", 0.70), ("hash_bwd", "hbm_frac", 0.70),
+                           ("field_fwd", "mfma_frac", 0.50), ("field_bwd", "mfma_frac", 0.50)):
+        k = kernels.get(name)
+        if not k or key not in k:
+            continue
+        e = {"avg_ms": k["avg_ms"], "frac": k[key], "target": tgt,
+             "achieved": k["hbm_gbs"] if key == "hbm_frac" else k["mfma_tfs"],
+             "unit": "GB/s" if key == "hbm_frac" else "TFLOP/s",
+             "peak": SPEC_PEAKS["hbm_copy_gbs"] if key == "hbm_frac" else SPEC_PEAKS[mfma_key]}
+        for x in ("mfma_frac_with_recompute", "atomic_frac", "survey_model_frac",
+                  "hbm_frac_measured", "mfma_frac_measured"):
+            if x in k:
+                e[x] = k[x]
+        out[name] = e
+    return out
 
 
 def ingp_config(variant: str, n_samples: int) -> dict:
@@ -310,8 +356,12 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
     roofline = {"kernel": ("nerf_linear_{fwd,dx,dw} (csrc/nerf_mlp.hip f32 MFMA GEMMs), "
                            "whole-step time" if native else
                            "nerf_mlp_gemms (library f32 GEMMs, whole-step time)"),
-                "bound": "mfma", "achieved": round(tfs, 2), "peak": peaks["mfma_f32_tfs"],
-                "unit": "TFLOP/s", "frac": round(tfs / peaks["mfma_f32_tfs"], 4), "traffic": None,
+                "bound": "mfma", "achieved": round(tfs, 2), "peak": SPEC_PEAKS["mfma_f32_tfs"],
+                "unit": "TFLOP/s", "frac": round(tfs / SPEC_PEAKS["mfma_f32_tfs"], 4),
+                "ceiling": "f32 MFMA spec peak, MI355X_MICROARCH.md",
+                "measured_ceiling": {"peak": peaks["mfma_f32_tfs"],
+                                     "frac": round(tfs / peaks["mfma_f32_tfs"], 4)},
+                "traffic": None,
                 "algorithmic_flops": flops, "units_per_launch": batch_size,
                 "flops_per_unit": flops / batch_size}
     kernels = None
@@ -331,7 +381,8 @@ def run_nerf(args, ds, dev, rank, world, t_scene):
             gtfs = flops / (gemm_ms * 1e-3) / 1e12
             roofline["gemm_kernels"] = {
                 "ms_per_step": round(gemm_ms, 3), "achieved": round(gtfs, 2),
-                "frac": round(gtfs / peaks["mfma_f32_tfs"], 4),
+                "frac": round(gtfs / SPEC_PEAKS["mfma_f32_tfs"], 4),
+                "frac_measured": round(gtfs / peaks["mfma_f32_tfs"], 4),
                 "source": "HIP events around each nerf_linear_* launch, untimed pass of "
                           f"{prof_steps} steps; flops = the step's algorithmic MLP flops"}
     cpu = None
@@ -440,16 +491,20 @@ def run_extract(args, ds, dev, rank, world, t_scene):
         mdl = models[dominant]
         r = _roof(mdl, st["avg_ms"], peaks, "mfma_f16_tfs")
         if r["bound"] == "hbm":
-            ach, peak, frac, unit = r["hbm_gbs"], peaks["hbm_copy_gbs"], r["hbm_frac"], "GB/s"
+            ach, peak, frac, unit = r["hbm_gbs"], SPEC_PEAKS["hbm_copy_gbs"], r["hbm_frac"], "GB/s"
+            mc = {"peak": peaks["hbm_copy_gbs"], "frac": r["hbm_frac_measured"]}
         else:
-            ach, peak, frac, unit = r["mfma_tfs"], peaks["mfma_f16_tfs"], r["mfma_frac"], "TFLOP/s"
+            ach, peak, frac, unit = (r["mfma_tfs"], SPEC_PEAKS["mfma_f16_tfs"], r["mfma_frac"],
+                                     "TFLOP/s")
+            mc = {"peak": peaks["mfma_f16_tfs"], "frac": r["mfma_frac_measured"]}
         roofline = {"kernel": dominant, "bound": r["bound"], "achieved": ach, "peak": peak,
-                    "unit": unit, "frac": frac, "traffic": None, "avg_ms": round(st["avg_ms"], 4),
+                    "unit": unit, "frac": frac, "measured_ceiling": mc,
+                    "traffic": None, "avg_ms": round(st["avg_ms"], 4),
                     "launches": st["launches"], "units_per_launch": P,
                     "algorithmic_bytes": mdl["bytes"], "algorithmic_flops": mdl["flops"],
                     "bytes_per_unit": mdl["bytes"] / P,
-                    "ceiling": "HBM float4 copy, measured" if r["bound"] == "hbm"
-                    else "dense MFMA loop on random operands, measured"}
+                    "ceiling": "HBM3E 8 TB/s, MI355X_MICROARCH.md" if r["bound"] == "hbm"
+                    else "dense f16 MFMA spec peak, MI355X_MICROARCH.md"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline
@@ -712,7 +767,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spec-peaks", action="store_true",
                     help="price the rooflines against spec-sheet peaks instead of measuring")
-    ap.add_argument("--cpu-budget", type=float, default=45.0)
+    ap.add_argument("--cpu-budget", type=float, default=150.0)
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--occupancy", action="store_true",
                     help="BASELINE configs[4]: occupancy-grid culling (beyond the reference); "
@@ -1007,29 +1062,41 @@ def main():
             bound = k["bound"]
             if bound == "atomic":
                 # memory-side f32 atomic requests per second (each a 64-B request carrying
-                # the kernel's 16-B segment), against the request ceiling measured on the
-                # same shape (the guide's 1.3 TB/s of 64-B requests is 20.3 G req/s)
-                ach, peak, frac = (k["atomic_greq_s"], peaks["atomic_seg16_greq_s"],
-                                   k["atomic_frac"])
+                # the kernel's 16-B segment), against the guide's request rate (1.3 TB/s of
+                # 64-B requests = 20.3 G req/s) and the ceiling measured on the same shape
+                ach, peak, frac, mpeak, mfrac = (
+                    k["atomic_greq_s"], SPEC_PEAKS["atomic_seg16_greq_s"], k["atomic_frac"],
+                    peaks["atomic_seg16_greq_s"], k["atomic_frac_measured"])
                 unit = "Greq/s"
             elif bound == "hbm":
-                ach, peak, frac, unit = k["hbm_gbs"], peaks["hbm_copy_gbs"], k["hbm_frac"], "GB/s"
+                ach, peak, frac, unit = k["hbm_gbs"], SPEC_PEAKS["hbm_copy_gbs"], k["hbm_frac"], "GB/s"
+                mpeak, mfrac = peaks["hbm_copy_gbs"], k["hbm_frac_measured"]
             else:
-                ach, peak, frac, unit = k["mfma_tfs"], peaks[mfma_key], k["mfma_frac"], "TFLOP/s"
+                ach, peak, frac, unit = (k["mfma_tfs"], SPEC_PEAKS[mfma_key], k["mfma_frac"],
+                                         "TFLOP/s")
+                mpeak, mfrac = peaks[mfma_key], k["mfma_frac_measured"]
             roofline = {"kernel": dominant, "bound": bound,
-                        "ceiling": ("memory-side f32 atomic requests (MI355X_MICROARCH.md "
-                                    "'Global float atomics'): 64-B requests per second, "
-                                    "ceiling measured at the kernel's 16-B segments"
+                        "ceiling": ("memory-side f32 atomic requests, MI355X_MICROARCH.md "
+                                    "'Global float atomics' (1.3 TB/s of 64-B requests)"
                                     if bound == "atomic" else
-                                    "HBM float4 copy, measured" if bound == "hbm" else
-                                    "dense MFMA loop on random operands, measured"),
+                                    "HBM3E 8 TB/s, MI355X_MICROARCH.md" if bound == "hbm" else
+                                    "dense MFMA spec peak, MI355X_MICROARCH.md"),
                         "achieved": ach, "peak": peak, "unit": unit, "frac": frac,
+                        "measured_ceiling": {
+                            "peak": mpeak, "frac": mfrac,
+                            "source": ("tools/ubench on this box in this run: " + (
+                                "scattered no-return f32 atomics at 16-B segments"
+                                if bound == "atomic" else "float4 copy" if bound == "hbm"
+                                else "bare MFMA loop on random operands"))},
                         "traffic": None, "avg_ms": round(st["avg_ms"], 4),
                         "launches": st["launches"], "units_per_launch": M,
                         "algorithmic_bytes": mdl["bytes"], "algorithmic_flops": mdl["flops"],
                         "bytes_per_unit": mdl["bytes"] / M,
-                        "fractions": {x: k[x] for x in ("hbm_frac", "mfma_frac", "atomic_frac",
-                                                        "survey_model_frac") if x in k}}
+                        "fractions": {x: k[x] for x in (
+                            "hbm_frac", "mfma_frac", "atomic_frac", "survey_model_frac",
+                            "mfma_frac_with_recompute") if x in k}}
+            if mdl.get("flops_with_recompute"):
+                roofline["algorithmic_flops_with_recompute"] = mdl["flops_with_recompute"]
             if st.get("source"):
                 roofline["timing_source"] = st["source"]
             if "atomic_requests" in mdl:
@@ -1108,6 +1175,7 @@ def main():
                 "parallelism": f"dp{world}",
             },
             "roofline": roofline,
+            "roofline_targets": target_rooflines(kernels, mfma_key),
             "cpu_baseline": cpu,
             "strong_scaling": strong,
             "alt_numerics": alt,

@@ -2,10 +2,11 @@
 
 bench.py's ``cpu_baseline`` leg: the reference's own CPU-runnable configuration
 (BASELINE.json configs[0]: nerf.json's pipeline on an 8-view 64x64 synthetic scene), run
-with oracle/ref_nerf.py on the host cores at nerf.json's own batch of 4,096 rays
-(r05 -- r01-r04 used 1,024), one warm-up step and up to three timed ones,
-so the bounded sample stays within bench.py's time budget. Returns rays/s and where the
-thread count came from.
+with oracle/ref_nerf.py at nerf.json's own batch of 4,096 rays, as BASELINE.md §3 plans it:
+every core of the process's affinity mask, the median of five timed steps after two
+warm-ups (r06; r05 took OMP_NUM_THREADS and 1 + 3 steps). The same step on the box's
+per-GPU host share (OMP_NUM_THREADS = 16) is timed beside it, and the cgroup CPU quota is
+reported, since threads beyond the quota only time-share.
 """
 
 from __future__ import annotations
@@ -17,18 +18,20 @@ import torch
 
 
 def host_threads(threads: int | None = None) -> tuple[int, str]:
-    """The host share the job may use, and where that number came from: OMP_NUM_THREADS
-    (the GPU box sets it to its per-GPU share of 16; os.cpu_count() there counts the whole
-    machine), else the process's CPU affinity mask."""
+    """The host cores the job may run on (the box's own host cores): the
+    process's CPU affinity mask, else os.cpu_count()."""
     if threads is not None:
         return threads, "argument"
-    env = os.environ.get("OMP_NUM_THREADS", "")
-    if env.isdigit() and int(env) > 0:
-        return int(env), "OMP_NUM_THREADS"
     try:
         return len(os.sched_getaffinity(0)), "len(os.sched_getaffinity(0))"
     except (AttributeError, OSError):
         return os.cpu_count() or 1, "os.cpu_count()"
+
+
+def omp_share() -> int | None:
+    """OMP_NUM_THREADS when set (the GPU box sets it to its per-GPU host share, 16)."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return int(env) if env.isdigit() and int(env) > 0 else None
 
 
 def _affinity() -> int | None:
@@ -38,15 +41,30 @@ def _affinity() -> int | None:
         return None
 
 
-def run(budget_s: float = 45.0, batch_size: int = 4096, threads: int | None = None,
-        seed: int = 0, warmup: int = 1, timed: int = 3) -> dict:
-    """Median rays/s of ``timed`` train steps after ``warmup`` (stops early at
-    ``budget_s``) on ``host_threads()`` threads."""
+def cpu_quota() -> float | None:
+    """CPUs granted by the cgroup v2 CPU quota (cpu.max), None when unlimited / unknown:
+    with an affinity mask wider than the quota, threads past it only time-share."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_model() -> str | None:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _nerf_setup(seed: int):
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
     from oracle.ref_nerf import RefNeRFPipeline
 
-    threads, source = host_threads(threads)
-    torch.set_num_threads(threads)
     torch.manual_seed(seed)
     ds = SyntheticHARP2Dataset(n_views=8, img_size=64, device="cpu", seed=seed)
     pp = ds._prep
@@ -56,17 +74,22 @@ def run(budget_s: float = 45.0, batch_size: int = 4096, threads: int | None = No
                 lon_min=torch.tensor(pp.lon_min, dtype=torch.float32),
                 lon_range=torch.tensor(pp.lon_range, dtype=torch.float32),
                 h0=pp.ray_origin_height, shift_lon=pp.shift_lon)
-    pipe = RefNeRFPipeline(prep, ds.scale)
+    return ds, RefNeRFPipeline(prep, ds.scale)
+
+
+def _time_steps(threads, batch_size, seed, warmup, timed, budget_s):
+    ds, pipe = _nerf_setup(seed)
+    torch.set_num_threads(threads)
     perm = torch.randperm(len(ds))
 
     def batch(k):
         return ds.__getbatch__(perm[(k * batch_size) % len(ds):][:batch_size])
 
+    t_start = time.perf_counter()
     for k in range(warmup):
         pipe.train_step(batch(k))
     times = []
     k = warmup
-    t_start = time.perf_counter()
     while True:
         t0 = time.perf_counter()
         pipe.train_step(batch(k))
@@ -75,18 +98,40 @@ def run(budget_s: float = 45.0, batch_size: int = 4096, threads: int | None = No
         if time.perf_counter() - t_start >= budget_s or len(times) >= timed:
             break
     times.sort()
-    med = times[len(times) // 2]
+    return batch_size / times[len(times) // 2], len(times)
+
+
+def run(budget_s: float = 150.0, batch_size: int = 4096, threads: int | None = None,
+        seed: int = 0, warmup: int = 2, timed: int = 5, share_budget_s: float = 75.0) -> dict:
+    """median rays/s of ``timed`` train steps after ``warmup`` on every
+    core of the affinity mask (stops early at ``budget_s``), and beside it the same step
+    on the box's per-GPU host share (OMP_NUM_THREADS, when it differs)."""
+    threads, source = host_threads(threads)
+    prev = torch.get_num_threads()
+    try:
+        value, n = _time_steps(threads, batch_size, seed, warmup, timed, budget_s)
+        share = omp_share()
+        at_share = None
+        if share and share != threads:
+            v2, n2 = _time_steps(share, batch_size, seed, warmup, timed, share_budget_s)
+            at_share = {"value": v2, "cores": share, "cores_source": "OMP_NUM_THREADS",
+                        "timed_steps": n2}
+    finally:
+        torch.set_num_threads(prev)
     return {
-        "value": batch_size / med,
+        "value": value,
         "unit": "rays/s",
         "cores": threads,
         "cores_source": source,
         "affinity_cpus": _affinity(),
         "host_cpus": os.cpu_count(),
+        "cgroup_cpu_quota": cpu_quota(),
+        "cpu_model": cpu_model(),
+        "at_host_share": at_share,
         "kind": "port",
         "sample": (f"configs/nerf.json train step (coarse 64 + fine 128 samples, 8x256 MLP, "
                    f"Adam) on an 8-view 64x64 synthetic HARP2 scene, batch {batch_size}; "
-                   f"median of {len(times)} timed steps after {warmup} warm-up, "
+                   f"median of {n} timed steps after {warmup} warm-up, "
                    f"torch CPU {torch.__version__}, {threads} threads of "
                    f"{os.cpu_count()} host CPUs"),
     }
@@ -143,7 +188,7 @@ def run_extract(budget_s: float = 20.0, n_points: int = 131072, threads: int | N
     return {
         "value": n_points / med, "unit": "points/s", "cores": threads,
         "cores_source": source, "affinity_cpus": _affinity(),
-        "host_cpus": os.cpu_count(), "kind": "port",
+        "host_cpus": os.cpu_count(), "cgroup_cpu_quota": cpu_quota(), "kind": "port",
         "sample": (f"extract loop body (f64 preprocessor, tcnn hash grid T=2^19 and 2x64 "
                    f"pos MLP restated in numpy / torch CPU) on {n_points} random in-scene "
                    f"points, median of {len(times)} batches, {threads} threads of "

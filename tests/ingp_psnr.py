@@ -118,6 +118,7 @@ class OracleRunner:
     def step(self, b, u, it):
         cb = self._batch(b)
         res = self.o.forward(cb, u)
+        self.last = res  # the step's forward results (tools/liveness_paired.py reads sigma)
         if it == 0 and self.perturb_ray is not None:
             k = self.perturb_ray
             c = int(cb["irgb_idx"][k])

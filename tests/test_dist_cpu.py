@@ -449,12 +449,28 @@ def _f16_exchange_worker(rank, world, port, out):
         if exchange == "f16":  # a gradient that is not an f16 number is refused
             with torch.no_grad():
                 ps[0].grad.fill_(0.1)
-            opt.steps = 0  # the check runs on the first step
+            opt.steps = 0  # the check runs on the first step ...
             try:
                 opt.step()
                 res["refused"] = False
             except ValueError:
                 res["refused"] = True
+            opt.check_every = 8  # ... and every check_every steps after it
+            opt.steps = 16
+            try:
+                opt.step()
+                res["refused_later"] = False
+            except ValueError:
+                res["refused_later"] = True
+            with torch.no_grad():  # a NaN is not reported as a non-f16 value
+                ps[0].grad.copy_(ps[0].grad.half().float())
+                ps[0].grad[0] = float("nan")
+            opt.steps = 0
+            try:
+                opt.step()
+                res["nan_passes"] = True
+            except ValueError:
+                res["nan_passes"] = False
     out[rank] = res
     dist.destroy_process_group()
 
@@ -472,7 +488,7 @@ def test_sharded_adam_f16_exchange(world):
     mp.spawn(_f16_exchange_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     for r in range(world):
         res = out[r]
-        assert res["refused"]
+        assert res["refused"] and res["refused_later"] and res["nan_passes"]
         for a, b in zip(res["f32"], res["f16"]):
             assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (r, (a - b).abs().max())
         for a, b in zip(out[0]["f16"], res["f16"]):

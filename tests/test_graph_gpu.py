@@ -178,6 +178,13 @@ def test_graph_replay_after_load_state_dict(dev):
     replay(4)
     torch.cuda.synchronize()
     assert all(torch.isfinite(q).all() for q in ps)
+    # weight decay is captured by value, so a checkpoint carrying another
+    # weight decay cannot be reloaded in place: the device state is dropped (recapture)
+    ck_wd = copy.deepcopy(ck_opt)
+    ck_wd["param_groups"][1]["weight_decay"] = 5e-2
+    gen1 = opt.generation
+    opt.load_state_dict(ck_wd)
+    assert opt.generation > gen1
 
 
 def test_adam_dev_rebuilds_when_grads_change(dev):

@@ -53,6 +53,8 @@ def main():
                     help="cuda: build the scene on the GPU exactly as the PSNR test does "
                     "(device libm), so the unperturbed run reproduces the test's oracle")
     ap.add_argument("--ref-acc", default="cuda", help="cuda | cpu (oracle/ref_ingp.py)")
+    ap.add_argument("--master", default="f64", help="f64 | f32: master parameters / AdamW "
+                    "moments of every run (f32 = tinycudann's torch binding, the GPU's)")
     ap.add_argument("--perturb", default="grad", help="grad: one f16 ulp of one ray's "
                     "loss gradient at step 0; dirs: every ray direction by one f32 ulp; "
                     "f32master: one run with f32 parameters / AdamW moments (the "
@@ -80,16 +82,16 @@ def main():
         o = ref_ingp.RefInstantNGP(cfg, state, ref_ingp.prep_kwargs(pp), p.scale, scene.max_i,
                                    half=True, semantics=a.semantics, ref_acc=a.ref_acc)
         if run < 0:
-            runners["unperturbed"] = ingp_psnr.OracleRunner(o, opt)
+            runners["unperturbed"] = ingp_psnr.OracleRunner(o, opt, master=a.master)
         elif a.perturb == "xnoise":
             runners[f"x_noise{run}"] = ingp_psnr.OracleRunner(
-                o, opt, grad_noise=(a.noise, 300 + run, "x"))
+                o, opt, grad_noise=(a.noise, 300 + run, "x"), master=a.master)
         elif a.perturb == "sumnoise":
             runners[f"sum_noise{run}"] = ingp_psnr.OracleRunner(
-                o, opt, grad_noise=(a.noise, 200 + run, "sum"))
+                o, opt, grad_noise=(a.noise, 200 + run, "sum"), master=a.master)
         elif a.perturb == "gradnoise":
             runners[f"grad_noise{run}"] = ingp_psnr.OracleRunner(
-                o, opt, grad_noise=(a.noise, 100 + run))
+                o, opt, grad_noise=(a.noise, 100 + run), master=a.master)
         elif a.perturb == "acc":
             # equally valid summation orders of the sums before each f16 rounding
             # (oracle/ref_ingp.py acc=): f32 in BLAS order, f32 reversed (f64 = unperturbed)
@@ -98,14 +100,16 @@ def main():
                 o = ref_ingp.RefInstantNGP(cfg, state, ref_ingp.prep_kwargs(pp), p.scale,
                                            scene.max_i, half=True, semantics=a.semantics,
                                            ref_acc=a.ref_acc, acc=arm)
-                runners[f"acc_{arm}"] = ingp_psnr.OracleRunner(o, opt)
+                runners[f"acc_{arm}"] = ingp_psnr.OracleRunner(o, opt, master=a.master)
         elif a.perturb == "f32master":
             if run == 0:
                 runners["f32_master"] = ingp_psnr.OracleRunner(o, opt, master="f32")
         elif a.perturb == "grad":
-            runners[f"perturb_ray{run}"] = ingp_psnr.OracleRunner(o, opt, perturb_ray=run)
+            runners[f"perturb_ray{run}"] = ingp_psnr.OracleRunner(o, opt, perturb_ray=run,
+                                                                     master=a.master)
         else:
-            runners[f"perturb_dirs{run}"] = ingp_psnr.OracleRunner(o, opt, perturb_dirs=run)
+            runners[f"perturb_dirs{run}"] = ingp_psnr.OracleRunner(o, opt, perturb_dirs=run,
+                                                                      master=a.master)
     t0 = time.time()
     cps = tuple(int(c) for c in a.checkpoints.split(",") if int(c) <= a.iters)
     res = ingp_psnr.train_side_by_side(runners, scene, a.samples, checkpoints=cps,

@@ -324,17 +324,21 @@ class _ReferenceRunner:
         self.step, self.render = self.r.step, self.r.render
 
 
-# Past this many iterations at 1,024 samples per ray (64 rays per step) training is chaotic:
-# in the test's exact configuration (profiles/r05_psnr_chaos_n1024.md) a one-ulp change of
-# every ray direction moves the oracle's own 64-iteration PSNR by -0.33 dB, the oracle's
-# f32 summation arm by -0.07 dB, and four GPU runs from identical inputs -- which differ only
-# in the order of the hash-grid backward's f32 atomic adds, as tinycudann's runs do -- span
-# 0.25 dB (17.86-18.11), while through 32 iterations every one of them agrees within 0.01 dB.
-# Past the horizon the bar compares the two outcome sets: the oracle's (reference semantics,
-# its f32 summation arm, every ray direction one ulp off: the reference's own run-to-run
-# freedom) and the GPU's (REPLICAS runs from the same inputs).
+# Past this many iterations at 1,024 samples per ray (64 rays per step) training is chaotic
+# (profiles/r05_psnr_chaos_n1024.md, profiles/r06_psnr_n1024_distribution.md): GPU runs from
+# identical inputs -- which differ only in the order of the hash-grid backward's f32 atomic
+# adds, as tinycudann's runs do -- spread by ~0.1 dB (sd) at 64 iterations, and a one-ulp
+# change of every ray direction moves the oracle by up to 0.25 dB, while through 32
+# iterations every one of them agrees within 0.01 dB. Past the horizon one run is one draw,
+# on either side, so the bar compares the two distributions' means: REPLICAS GPU runs
+# against the oracle's ORACLE_ARMS, reference semantics with f32 master parameters as
+# tinycudann's torch binding (and the GPU) keep them -- unperturbed and with every ray
+# direction one f32 ulp off under three seeds. (The f64-master oracle of the strict checks
+# is recorded beside them; it sits at the top of that distribution at 64 iterations.)
 CHAOS_AFTER = {1024: 32}
-REPLICAS = 4
+REPLICAS = 16
+ORACLE_ARMS = (("oracle_f32_master", "f32", None), ("oracle_f32_master_dirs0", "f32", 0),
+               ("oracle_f32_master_dirs1", "f32", 1), ("oracle_f32_master_dirs2", "f32", 2))
 
 
 @pytest.mark.timeout(1200)
@@ -350,12 +354,12 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
     scene) and at the bench's 1,024. The north-star bar, 0.1 dB, holds at every
     checkpoint: at 64 samples per ray and at 1,024 through 32 iterations against the run
     itself. Beyond that (CHAOS_AFTER) one run's PSNR is one draw from a distribution, on
-    either side, so the bar applies to the two outcome sets: REPLICAS GPU runs from
-    identical inputs (the hash-grid backward's atomics order, as tinycudann's) and the
-    oracle's own arms (reference semantics; its f32 summation order; every ray direction
-    one ulp off, the size of host-vs-device libm differences): their nearest pair must
-    agree within 0.1 dB. Both sets are recorded. The build numerics' distance is recorded
-    beside it (a deliberate deviation: DESIGN.md §3.1). Training must gain >= 3 dB."""
+    either side, so the bar applies to the distributions' means: the mean of REPLICAS GPU
+    runs from identical inputs (the hash-grid backward's atomics order, as tinycudann's)
+    and the mean of the oracle's ORACLE_ARMS (f32 masters, as the reference's) agree
+    within 0.1 dB. Both sets, their means and spreads are recorded. The
+    build numerics' distance is recorded beside it (a deliberate deviation: DESIGN.md
+    §3.1). Training must gain >= 3 dB."""
     from tests.ingp_psnr import PipelineRunner, train_side_by_side
 
     p_ref, o = _pair(scene, dev, torch.float16, numerics="reference", n_samples=n_samples)
@@ -377,11 +381,11 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
             runners[replicas[-1]] = PipelineRunner(p_r, OPT, dev)
         cfg = ge._ingp_config(n_samples)
         pp = scene.get_point_preprocessor("horizontal")
-        for name, acc, dirs in (("oracle_f32_sums", "f32", None), ("oracle_dirs_ulp", "f64", 0)):
+        for name, master, dirs in ORACLE_ARMS:
             oa = ref_ingp.RefInstantNGP(cfg, p_ref._anr_initial_state, ref_ingp.prep_kwargs(pp),
                                         p_ref.scale, scene.max_i, half=True,
-                                        semantics="reference", acc=acc)
-            runners[name] = OracleRunner(oa, OPT, perturb_dirs=dirs)
+                                        semantics="reference")
+            runners[name] = OracleRunner(oa, OPT, perturb_dirs=dirs, master=master)
             arms.append(name)
     key = "psnr_reference_semantics" + ("" if n_samples == N else f"_n{n_samples}")
     out = train_side_by_side(runners, scene, n_samples, checkpoints=checkpoints, batch=batch,
@@ -395,10 +399,13 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
         row["delta_build_db"] = row["psnr_gpu_build"] - r["psnr"]
         if replicas:
             runs = [row["psnr_gpu_reference_numerics"]] + [out[k][i]["psnr"] for k in replicas]
-            oracles = [r["psnr"]] + [out[k][i]["psnr"] for k in arms]
+            oracles = [out[k][i]["psnr"] for k in arms]
             row["psnr_gpu_replicas"] = runs
             row["psnr_oracle_arms"] = oracles
-            row["delta_replicas_db"] = [v - r["psnr"] for v in runs]
+            row["oracle_arm_names"] = arms
+            row["gpu_mean"] = sum(runs) / len(runs)
+            row["oracle_mean"] = sum(oracles) / len(oracles)
+            row["delta_means_db"] = row["gpu_mean"] - row["oracle_mean"]
             row["replica_spread_db"] = max(runs) - min(runs)
             row["oracle_arm_spread_db"] = max(oracles) - min(oracles)
             row["nearest_pair_db"] = min(abs(u - v) for u in runs for v in oracles)
@@ -411,7 +418,7 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
         if horizon is None or row["iteration"] <= horizon:
             assert abs(row["delta_reference_numerics_db"]) <= 0.1, rows
         else:
-            assert row["nearest_pair_db"] <= 0.1, rows
+            assert abs(row["delta_means_db"]) <= 0.1, rows
     assert rows[-1]["psnr_oracle"] > rows[0]["psnr_oracle"] + 3.0, rows
 
 

@@ -12,9 +12,10 @@ gradient through sample_pdf's t_in_bin (samplers.py:92-96) divides by the cdf wi
 bin a fine sample lands in, so a perturbation of the coarse weights by one f32 rounding
 (1e-7 relative) moves the coarse gradient by ~4 % (measured on the oracle alone). Hence two
 checks:
-* strict: that gradient path detached in both runs (everything else identical) — after
-  16 Adam steps PSNR within 0.1 dB and last-batch loss (128 rays) within 5 % (the fine samples still move with the
-  coarse weights' last bits, so the runs drift slowly apart; 7+ dB of training progress);
+* strict: that gradient path detached in both runs (everything else identical), over
+  PERMS summation orders per side (hidden units permuted: same mathematics) — the mean
+  PSNR after 16 Adam steps within 0.1 dB, every pair's last-batch loss within 5 % (7+ dB
+  of training progress);
 * reference semantics (path attached): the GPU run must land within the spread of oracle
   runs whose fine-sampler weights are perturbed by one f32 rounding.
 With ANR_PSNR_OUT set, the numbers are written there as JSON (profiles/ records them).
@@ -121,9 +122,35 @@ def _setup(dev):
     return scene
 
 
-def _train(dev, scene, K, gpu, detach_pdf, perturb_seed=None, lr=5e-4):
+def permute_hidden(sd: dict, seed: int) -> dict:
+    """An AtmoNeRF state dict with the hidden units of every layer (fc1-fc8's 256, fc9's
+    first 256, fc10's 128) permuted, and the next layer's input columns with them: the
+    same network to the last bit of its exact arithmetic, with every dot product summed
+    in another order. Adam is elementwise, so training is permutation-equivariant too: a
+    permutation arm samples the run-to-run freedom of the GEMM summation order (as two
+    BLAS libraries differ) without changing the mathematics."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {k: v.detach().clone() for k, v in sd.items()}
+    h = sd["fc1.weight"].shape[0]
+    for i in range(1, 11):
+        n_hidden = h if i <= 9 else sd["fc10.weight"].shape[0]
+        p = torch.randperm(n_hidden, generator=g).to(sd[f"fc{i}.weight"].device)
+        full = torch.arange(sd[f"fc{i}.weight"].shape[0], device=p.device)
+        full[:n_hidden] = p  # fc9's density rows stay in place
+        sd[f"fc{i}.weight"] = sd[f"fc{i}.weight"][full]
+        sd[f"fc{i}.bias"] = sd[f"fc{i}.bias"][full]
+        nxt = {9: 10, 10: 11}.get(i, i + 1)
+        w = sd[f"fc{nxt}.weight"]
+        cols = torch.arange(w.shape[1], device=p.device)
+        cols[:n_hidden] = p  # fc6's skip and fc10's direction columns stay in place
+        sd[f"fc{nxt}.weight"] = w[:, cols]
+    return sd
+
+
+def _train(dev, scene, K, gpu, detach_pdf, perturb_seed=None, lr=5e-4, permute_seed=None):
     """Train either the GPU pipeline or the oracle from the same init (seed 0) on the same
-    batches and draws; return [(iteration, loss, PSNR)] at the iterations in K."""
+    batches and draws; return [(iteration, loss, PSNR)] at the iterations in K.
+    ``permute_seed``: both networks' hidden units permuted first (permute_hidden)."""
     from atmonr_amd.batch_loader import BatchLoader
     from atmonr_amd.pipelines.factory import get_pipeline
     import atmonr_amd.pipelines.nerf as nmod
@@ -131,6 +158,9 @@ def _train(dev, scene, K, gpu, detach_pdf, perturb_seed=None, lr=5e-4):
     torch.manual_seed(0)
     pipe = get_pipeline(CFG, scene)
     pipe.send_tensors_to(dev)
+    if permute_seed is not None:
+        pipe.load_state_dict({m: permute_hidden(s, 1000 * permute_seed + j)
+                              for j, (m, s) in enumerate(pipe.state_dict().items())})
     pipe.eval()  # density noise off
     pp = scene.get_point_preprocessor("horizontal")
     orig_dev, orig_ref = nmod.sample_pdf, ref_nerf.sample_pdf
@@ -196,34 +226,43 @@ def _dump():
 
 # CPU oracle training dominates these tests (minutes on a GPU box's host share): the
 # per-test limit is raised above the suite's --timeout.
+PERMS = 8
+
+
 @pytest.mark.timeout(900)
 def test_psnr_at_fixed_iterations_strict(dev):
-    """t_in_bin gradient detached in both: the two implementations track each other. A
-    NeRF run at this scale is itself a draw: a 1e-7 relative perturbation of the coarse
-    weights entering the pdf sampler moves either side's 16-iteration PSNR by ~0.1 dB, one
-    f32 rounding of the weights by up to 0.7 dB (the full-gradient test below), and the
-    GPU's GEMM summation order is as free as the reference's cuBLAS one (hipBLASLt -0.02
-    dB, the r05 f32 MFMA kernels +0.12 dB from the unperturbed oracle). So the bar applies
-    to the two outcome sets, three GPU runs and four oracle runs (unperturbed and
-    perturbed alike on both sides): their nearest pair within 0.1 dB at every checkpoint,
-    all recorded."""
+    """t_in_bin gradient detached in both. A NeRF run at this scale is itself a draw from
+    the summation order of its GEMMs: 1e-7 relative perturbations of the pdf weights
+    spread one side's 16-iteration PSNR by ~0.12 dB, and so does changing the order in
+    which every dot product is summed -- the freedom two BLAS libraries have. The bar
+    therefore applies to distributions over that freedom: both sides train PERMS times,
+    each time with the hidden units of both networks permuted by the same permutation
+    (permute_hidden: the same mathematics, every dot product summed in another order),
+    and the mean PSNR over the GPU runs and over the oracle runs must agree within 0.1 dB
+    at every checkpoint; each pair's last-batch loss (128 rays) within 5 %. Measured
+    (profiles/r06_nerf_psnr_permutations.md): native kernels 15.846, library GEMMs
+    15.864, oracle 15.838 dB, while the unpermuted pair alone sits 0.12 dB apart -- one
+    draw, not an offset: a native-forward/library-backward hybrid lands with the native
+    runs, and both forwards render the same weights to the same PSNR bit for bit."""
     scene = _setup(dev)
     K = KS
     _REC["iterations"] = K
-    g = _train(dev, scene, K, gpu=True, detach_pdf=True)
-    gpus = [g] + [_train(dev, scene, K, gpu=True, detach_pdf=True, perturb_seed=s)
-                  for s in (1, 2)]
-    o = _train(dev, scene, K, gpu=False, detach_pdf=True)
-    arms = [o] + [_train(dev, scene, K, gpu=False, detach_pdf=True, perturb_seed=s)
-                  for s in (1, 2, 3)]
-    _REC["strict"] = {"gpu": g, "gpu_perturbed": gpus[1:], "oracle": o,
-                      "oracle_perturbed": arms[1:]}
+    gpus = [_train(dev, scene, K, gpu=True, detach_pdf=True, permute_seed=p)
+            for p in range(PERMS)]
+    arms = [_train(dev, scene, K, gpu=False, detach_pdf=True, permute_seed=p)
+            for p in range(PERMS)]
+    means = [{"iteration": K[i], "gpu_mean": sum(r[i][2] for r in gpus) / PERMS,
+              "oracle_mean": sum(a[i][2] for a in arms) / PERMS} for i in range(len(K))]
+    for m in means:
+        m["delta_means_db"] = m["gpu_mean"] - m["oracle_mean"]
+    _REC["strict"] = {"gpu_permutations": gpus, "oracle_permutations": arms, "means": means}
     _dump()
-    for i, (_, lg, pg) in enumerate(g):
-        assert min(abs(r[i][2] - a[i][2]) for r in gpus for a in arms) < 0.1, _REC
-        if lg == lg:  # not NaN (iteration 0 has no loss)
-            assert abs(lg - o[i][1]) < 5e-2 * o[i][1], _REC
-    assert g[-1][2] > g[0][2] + 1.0, _REC
+    for i, m in enumerate(means):
+        assert abs(m["delta_means_db"]) < 0.1, _REC
+        for g, o in zip(gpus, arms):
+            if g[i][1] == g[i][1]:  # not NaN (iteration 0 has no loss)
+                assert abs(g[i][1] - o[i][1]) < 5e-2 * o[i][1], _REC
+    assert means[-1]["gpu_mean"] > means[0]["gpu_mean"] + 1.0, _REC
 
 
 @pytest.mark.timeout(900)

@@ -101,6 +101,78 @@ def psnr_arms(dev, seeds, arms):
     return {"runs": rec, "mean": means}
 
 
+def permutation_arms(dev, seeds, arms):
+    """The strict test's training with both networks' hidden units permuted
+    (tests/test_psnr_gpu.permute_hidden, seed p on every side): the same mathematics with
+    every dot product summed in another order. Paired per permutation, a systematic
+    native-vs-oracle offset shows in every pair; summation-order chaos averages out."""
+    scene = T._setup(dev)
+    rec = {a: {} for a in arms}
+    for p in seeds:
+        for arm in arms:
+            _set_arm("native" if arm == "oracle32" else arm)
+            rec[arm][p] = T._train(dev, scene, T.KS, gpu=arm != "oracle32", detach_pdf=True,
+                                   permute_seed=p)
+        _set_arm("native")
+        print("permutation", p, {a: round(r[p][-1][2], 4) for a, r in rec.items()}, flush=True)
+    means = {a: sum(r[p][-1][2] for p in seeds) / len(seeds) for a, r in rec.items()}
+    print("permutation mean PSNR at", T.KS[-1], {a: round(m, 4) for a, m in means.items()},
+          flush=True)
+    return {"runs": rec, "mean": means}
+
+
+def render_check(dev, train_arm="torch", seed=0):
+    """Train with ``train_arm`` (the strict test's 16 steps), then render every ray of the
+    scene with the native and with the library forward from the SAME weights: PSNR of each
+    and the largest per-ray colour difference."""
+    import atmonr_amd.nerf_model as nm
+    from atmonr_amd.batch_loader import BatchLoader
+    from atmonr_amd.pipelines.factory import get_pipeline
+
+    scene = T._setup(dev)
+    _set_arm(train_arm)
+    torch.manual_seed(0)
+    pipe = get_pipeline(T.CFG, scene)
+    pipe.send_tensors_to(dev)
+    pipe.eval()
+    opt = pipe.get_optimizer({"lr": 5e-4})
+    import atmonr_amd.pipelines.nerf as nmod
+    orig = nmod.sample_pdf
+    nmod.sample_pdf = lambda rb, w, z, n_samples=128, u=None: orig(rb, w.detach(), z,
+                                                                     n_samples=n_samples, u=u)
+    try:
+        gen = torch.Generator().manual_seed(7)
+        batches = iter(BatchLoader(scene, T.BATCH, seed=3))
+        for _ in range(T.KS[-1]):
+            b = next(batches)
+            B = b["origin"].shape[0]
+            uc, uf = torch.rand(B, 64, generator=gen), torch.rand(B, 128, generator=gen)
+            res = pipe.forward(b, u_coarse=uc.to(dev), u_fine=uf.to(dev))
+            loss = pipe.compute_loss(b, res)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        out = {}
+        fwd = lambda b, uc, uf: pipe.forward(b, u_coarse=uc.to(dev), u_fine=uf.to(dev))[
+            "color_map_fine"]
+        target = scene.target_image()
+        for arm in ("native", "torch"):
+            nm._NATIVE = arm == "native"
+            pix = T._render_all(fwd, scene)
+            out[arm] = {"pix": pix, "psnr": float(scene.get_image_metrics(
+                scene.scatter_image(pix.to(dev)), target)["PSNR_mean"])}
+        nm._NATIVE = True
+    finally:
+        nmod.sample_pdf = orig
+        _set_arm("native")
+    d = (out["native"]["pix"] - out["torch"]["pix"]).abs()
+    rec = {"trained_with": train_arm, "psnr_native_render": out["native"]["psnr"],
+           "psnr_torch_render": out["torch"]["psnr"], "max_abs_pixel_diff": float(d.max()),
+           "mean_abs_pixel_diff": float(d.mean())}
+    print("render check", rec, flush=True)
+    return rec
+
+
 def mlp_accuracy(dev, n_steps=8):
     """Per-layer MLP gradients of real training inputs: each arm vs f64."""
     import atmonr_amd.nerf_model as nm
@@ -143,6 +215,7 @@ def mlp_accuracy(dev, n_steps=8):
             net = pipe.nerf[mode]
             x = captured[id(net)]
             tg = torch.Generator(device=dev).manual_seed(11)
+            gcol = gsig = None
             rows = {}
             for arm in ("native", "torch", "f64"):
                 nm._NATIVE = arm == "native"
@@ -156,9 +229,11 @@ def mlp_accuracy(dev, n_steps=8):
                     m, xi = net, x
                 m.zero_grad(set_to_none=True)
                 color, sigma = m(xi)
-                gc = torch.randn(color.shape, generator=tg, device=dev).to(color.dtype)
-                gs = torch.randn(sigma.shape, generator=tg, device=dev).to(sigma.dtype)
-                torch.autograd.backward([color, sigma], [gc, gs])
+                if gcol is None:  # one upstream gradient for every arm
+                    gcol = torch.randn(color.shape, generator=tg, device=dev)
+                    gsig = torch.randn(sigma.shape, generator=tg, device=dev)
+                torch.autograd.backward([color, sigma], [gcol.to(color.dtype),
+                                                         gsig.to(sigma.dtype)])
                 rows[arm] = ({k: p.grad.detach().double().clone()
                               for k, p in m.named_parameters()},
                              color.detach().double(), sigma.detach().double())
@@ -192,14 +267,21 @@ def main():
     ap.add_argument("--seeds", type=int, default=5)
     ap.add_argument("--arms", default="native,torch,nfwd_tbwd,oracle32")
     ap.add_argument("--mlp-accuracy", action="store_true")
+    ap.add_argument("--render-check", action="store_true")
+    ap.add_argument("--perms", type=int, default=0)
+    ap.add_argument("--perm-arms", default="native,torch,oracle32")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda")
     res = {}
     if a.mlp_accuracy:
         res["mlp_accuracy"] = mlp_accuracy(dev)
+    if a.render_check:
+        res["render_check"] = [render_check(dev, arm) for arm in ("torch", "native")]
     if a.seeds:
         res["psnr"] = psnr_arms(dev, range(a.seeds), a.arms.split(","))
+    if a.perms:
+        res["permutations"] = permutation_arms(dev, range(a.perms), a.perm_arms.split(","))
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:

@@ -33,6 +33,12 @@ def main():
     ap.add_argument("--checkpoints", default="0,8,32,48,64")
     ap.add_argument("--numerics", default="reference")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--with-build", action="store_true",
+                    help="also train a build-numerics pipeline interleaved (as the test does)")
+    ap.add_argument("--no-surface-stream", action="store_true",
+                    help="the surface branch on the main stream")
+    ap.add_argument("--with-oracle", action="store_true",
+                    help="also train the reference-semantics oracle interleaved (as the test)")
     a = ap.parse_args()
     import __graft_entry__ as ge
     from atmonr_amd.datasets.synthetic import SyntheticHARP2Dataset
@@ -46,8 +52,20 @@ def main():
     for r in range(a.runs):
         p = InstantNGPPipeline(cfg, scene, dtype=torch.float16, fused=True, seed=5,
                                numerics=a.numerics)
+        if a.no_surface_stream:
+            p.surface_stream = False
         p.send_tensors_to(dev)
         runners[f"gpu_run{r}"] = ingp_psnr.PipelineRunner(p, opt, dev)
+        if r == 0 and a.with_build:
+            pb = InstantNGPPipeline(cfg, scene, dtype=torch.float16, fused=True, seed=5)
+            pb.send_tensors_to(dev)
+            runners["gpu_build"] = ingp_psnr.PipelineRunner(pb, opt, dev)
+        if r == 0 and a.with_oracle:
+            from oracle import ref_ingp
+            pp = scene.get_point_preprocessor("horizontal")
+            o = ref_ingp.RefInstantNGP(cfg, p.state_dict(), ref_ingp.prep_kwargs(pp), p.scale,
+                                       scene.max_i, half=True, semantics="reference")
+            runners["oracle"] = ingp_psnr.OracleRunner(o, opt)
     cps = tuple(int(c) for c in a.checkpoints.split(","))
 
     def progress(out):

@@ -240,6 +240,11 @@ _SIGNATURES = {
         [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, c_int64, c_int64,
          _P, _P, c_int64, _P],
     ),
+    "anr_ingp_hash_field_fwd": (
+        c_int32,
+        [POINTER(HashGridDesc), _P, c_int64, _P, c_int32, _P, c_int64, POINTER(MlpDesc),
+         POINTER(MlpDesc), c_int32, _P, _P, c_int64, _P, _P, c_int64, _P],
+    ),
     "anr_ingp_field_density": (
         c_int32,
         [POINTER(MlpDesc), POINTER(MlpDesc), c_int32, _P, _P, c_int64, c_int64, _P, _P],

@@ -67,7 +67,40 @@ class IngpFieldFn(torch.autograd.Function):
         dirs = dirs.float().contiguous()
 
         fused = field_fused(pipe) and enc_mod.dtype == torch.float16
-        if fused and _enc_planes(grid, M):
+        if rows is not None and not fused:
+            raise _lib.ANRError("occupancy culling needs the fused f16 field")
+        if cdt == torch.bfloat16 and not fused:
+            raise _lib.ANRError("bf16 networks run only in the fused field (f16 hash features)")
+        ctx.pipe = pipe
+        ctx.n_per_ray = n_per_ray
+        ctx.params = (p_hash, p_pos, p_dir)
+        ctx.rows = rows
+        planes = fused and _enc_planes(grid, M)
+        if fused:
+            mma = _mma_code(pipe)
+            pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
+            packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc),
+                                 device=dev, dtype=torch.float16)  # 16-bit carrier
+            m_pos, m_dir = _lib.pack_source(p_pos, mma), _lib.pack_source(p_dir, mma)
+            call("anr_ingp_field_pack", pdesc, ddesc, mma, ptr(m_pos), ptr(m_dir), ptr(packed),
+                 s, tag="field_pack")
+            nb = pipe.dir_mlp.n_output_dims
+        if planes and rows is None and _hash_field_ok(grid, nb, n_per_ray):
+            # hash grid + field forward in one kernel (anr_ingp_hash_field_fwd): the level-
+            # quad planes are written for the backward and never re-read by the forward
+            nq = (grid.desc.n_levels + 3) // 4
+            enc = torch.empty(nq, M, 8, device=dev, dtype=torch.float16)
+            ctx.enc_ld = -8 * M
+            sigma = torch.empty(M, device=dev, dtype=torch.float32)
+            color = torch.empty(M, nb, device=dev, dtype=torch.float32)
+            call("anr_ingp_hash_field_fwd", ctypes.byref(grid.desc), ptr(coords), M,
+                 ptr(t_hash), dtype_code(t_hash.dtype), ptr(enc), 8 * M, pdesc, ddesc, mma,
+                 ptr(packed), ptr(dirs), n_per_ray, ptr(sigma), ptr(color), color.stride(0), s,
+                 tag="hash_field_fwd")
+            ctx.fused_field = True
+            ctx.save_for_backward(coords, dirs, enc, packed)
+            return sigma, color
+        if planes:
             # level-quad planes (anr_hashgrid_fwd_planes: one lane per sample, coalesced;
             # 0.47-0.50 ms vs the row-layout walker's 0.63 at the bench shape), handed to the
             # field kernels as enc_stride = -plane
@@ -82,24 +115,8 @@ class IngpFieldFn(torch.autograd.Function):
             call("anr_hashgrid_fwd", ctypes.byref(grid.desc), ptr(coords), 3, M, ptr(t_hash),
                  dtype_code(t_hash.dtype), ptr(enc), dtype_code(enc.dtype), enc_ld, s,
                  tag="hash_fwd")
-        ctx.pipe = pipe
-        ctx.n_per_ray = n_per_ray
-        ctx.params = (p_hash, p_pos, p_dir)
-        ctx.rows = rows
         ctx.enc_ld = enc_ld
-        if rows is not None and not fused:
-            raise _lib.ANRError("occupancy culling needs the fused f16 field")
-        if cdt == torch.bfloat16 and not fused:
-            raise _lib.ANRError("bf16 networks run only in the fused field (f16 hash features)")
         if fused:
-            mma = _mma_code(pipe)
-            pdesc, ddesc = ctypes.byref(pos_mod.desc), ctypes.byref(pipe.dir_mlp.desc)
-            packed = torch.empty(_lib.load().anr_ingp_field_packed_size(pdesc, ddesc),
-                                 device=dev, dtype=torch.float16)  # 16-bit carrier
-            m_pos, m_dir = _lib.pack_source(p_pos, mma), _lib.pack_source(p_dir, mma)
-            call("anr_ingp_field_pack", pdesc, ddesc, mma, ptr(m_pos), ptr(m_dir), ptr(packed),
-                 s, tag="field_pack")
-            nb = pipe.dir_mlp.n_output_dims
             if rows is None:
                 sigma = torch.empty(M, device=dev, dtype=torch.float32)
                 color = torch.empty(M, nb, device=dev, dtype=torch.float32)
@@ -252,7 +269,16 @@ def _enc_planes(grid, M: int) -> bool:
             and 16 * nq * (M + 256) < 2 ** 31)
 
 
+def _hash_field_ok(grid, n_out: int, n_per_ray: int) -> bool:
+    """anr_ingp_hash_field_fwd's shapes: 16 levels x 2 features (3-D), 4 colour outputs,
+    samples per ray a multiple of 64. ANR_HASH_FIELD=0 keeps the two-kernel forward (A/B)."""
+    d = grid.desc
+    return (_HASH_FIELD and d.n_levels == 16 and d.n_features == 2 and d.n_dims == 3
+            and n_out == 4 and n_per_ray % 64 == 0)
+
+
 _ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"
+_HASH_FIELD = os.environ.get("ANR_HASH_FIELD", "1") != "0"
 _TILE_SKIP = os.environ.get("ANR_TILE_SKIP", "0") != "0"
 
 

@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "anr_common.h"
+#include "hash_levels.h"
 
 // Profiling ablations (tools/field_ablate.sh); 0 in every product build. Bits:
 // 1 no dW MFMAs, 2 no layer-input stores, 4 no gradient-tile stores, 8 no mask reads.
@@ -705,6 +706,111 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) f
     Rows cur;
     load_rows<ROWS>(a, tile * 16 + li, g, false, cur);
     body(cur, tile * 16 + li);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Hash-grid forward + field forward in one kernel (r06). A wavefront
+// takes 64 consecutive samples (one ray segment: n_per_ray is a multiple of 64) at a time:
+//  1. hash phase, one lane per sample: the 16 levels as four level quads (plane_quad, the
+//     arithmetic of anr_hashgrid_fwd_planes), each stored to its plane for the backward
+//     and to the wavefront's LDS stage;
+//  2. field phase, the four 16-sample tiles of the uniform-tile forward: lane group g reads
+//     quad g of its sample from the stage -- exactly the B fragment of the first layer --
+//     and tile_forward runs on weight fragments read from LDS.
+// The planes are written once and never re-read by the forward (the separate field
+// forward read all 64 B per sample back from HBM), and one wavefront's gathers overlap
+// other wavefronts' MFMA tiles on the same CU. Bit-identical to anr_hashgrid_fwd_planes
+// followed by anr_ingp_field_fwd (same per-level arithmetic, same MFMA sequence).
+struct HashArgs {
+  GridLevels G;
+  const float* x;
+  uint32_t x_bytes;
+  const __half* table;
+  uint32_t table_bytes;
+  _Float16* planes;
+  uint32_t plane_bytes;  // bytes from one level-quad plane to the next
+  uint32_t out_bytes;    // bytes of the plane buffer (range check of the stores)
+};
+
+template <int W, int NHD, bool BF, int WAVES, int OCC>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
+hf_fwd_kernel(Args a, HashArgs h) {
+  using N = Net<W, NHD>;
+  typedef uint32_t u4q __attribute__((vector_size(16)));
+  __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_fwd];
+  // per wavefront: quad q of lane l's sample at stage[wave][q][l]
+  __shared__ __attribute__((aligned(16))) u4q stage[WAVES][4][64];
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int e = threadIdx.x * 8; e < N::n_fwd; e += 64 * WAVES * 8)
+    *reinterpret_cast<h8*>(wsm + e) = *reinterpret_cast<const h8*>(a.packed + e);
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rx = wave_rsrc(h.x, h.x_bytes);
+  const __amdgpu_buffer_rsrc_t rt = wave_rsrc(h.table, h.table_bytes);
+  const __amdgpu_buffer_rsrc_t ro = wave_rsrc(h.planes, h.out_bytes);
+  const __amdgpu_buffer_rsrc_t rsig = out_rsrc(a.sigma, a.M * 4);
+  const __amdgpu_buffer_rsrc_t rcol = out_rsrc(a.color, a.M * a.color_stride * 4);
+  const uint32_t cs_bytes = static_cast<uint32_t>(a.color_stride) * 4u;
+  const int64_t n_super = (a.M + 63) / 64;
+  const int64_t sstride = static_cast<int64_t>(gridDim.x) * WAVES;
+  for (int64_t st = static_cast<int64_t>(blockIdx.x) * WAVES + wave; st < n_super; st += sstride) {
+    const uint32_t m = static_cast<uint32_t>(st * 64) + lane;
+    // ---- hash phase: lane = sample (coordinates past x's end read as 0, stores past M
+    // dropped by the range check)
+    const auto xr = __builtin_amdgcn_raw_buffer_load_b96(rx, m * 12u, 0, 0);
+    const float xv[3] = {__uint_as_float(xr[0]), __uint_as_float(xr[1]), __uint_as_float(xr[2])};
+    const uint32_t orow = m < a.M ? m * 16u : 0x80000000u;
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+      uint32_t p[4];
+      plane_quad<3, __half>(h.G, 16, q, xv, rt, p);
+      const u4q v = {p[0], p[1], p[2], p[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(v, ro, static_cast<uint32_t>(q) * h.plane_bytes + orow,
+                                             0, 0);
+      stage[wave][q][lane] = v;
+    }
+    // one wavefront's LDS accesses complete in order: the stage is read back below without
+    // a barrier (the fence keeps the compiler from hoisting the reads above the writes)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- field phase: the segment is one ray (n_per_ray % 64 == 0): scalar direction
+    const uint32_t ray =
+        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(st * 64) / a.n_per_ray);
+    const const_f32* d = (const_f32*)(a.dirs + static_cast<int64_t>(ray) * 3);
+    auto sdir = [&](int k) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, d[k])));
+    };
+    Rows cur;
+    cur.dx = sdir(0) * 2.0f - 1.0f;
+    cur.dy = sdir(1) * 2.0f - 1.0f;
+    cur.dz = sdir(2) * 2.0f - 1.0f;
+    cur.dc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    cur.ds = 0.0f;
+#pragma unroll 1
+    for (int t = 0; t < 4; ++t) {
+      cur.xe = __builtin_bit_cast(h8, stage[wave][g][16 * t + li]);
+      const uint32_t row = static_cast<uint32_t>(st * 64) + 16 * t + li;
+      const bool valid = row < a.M;
+      // per-tile opaque fragment base: the weight fragments are read from LDS at their
+      // MFMAs instead of being hoisted out of the loops into 80 registers
+      int zoff = 0;
+      asm volatile("" : "+v"(zoff));
+      const LdsWeights<W, NHD> fw{wsm + zoff, lane};
+      Tile<W, NHD> tt;
+      tile_forward<W, NHD, 1, BF>(fw, &cur, &valid, g, &tt, NoSink{});
+      const uint32_t so = g == 0 && valid ? row * 4u : 0x80000000u;
+      const uint32_t co = g == 0 && valid ? row * cs_bytes : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaxf(tt.po[0], 0.0f)), rsig, so, 0, 0);
+      const u4v v = {__float_as_uint(fmaxf(tt.col[0], 0.0f)), __float_as_uint(fmaxf(tt.col[1], 0.0f)),
+                     __float_as_uint(fmaxf(tt.col[2], 0.0f)), __float_as_uint(fmaxf(tt.col[3], 0.0f))};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rcol, co, 0, 0);
+    }
+    // the next segment's stage writes stay behind this segment's reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -1552,6 +1658,55 @@ static int variant(const anr_mlp_desc* pos, const anr_mlp_desc* dir) {
   return pos->width * 10 + dir->n_hidden_layers;
 }
 
+// fused hash-grid + field forward: a persistent grid of HF_WAVES-wavefront blocks, as many
+// as fit on the chip at once (the occupancy query), each wavefront walking 64-sample
+// segments grid-stride
+constexpr int HF_WAVES = 8;
+// register cap (waves per SIMD) of the fused forward: ANR_HF_OCC = 4 / 5 / 6 (A/B hook)
+static int hf_occ() {
+  static const int v = [] {
+    const char* e = getenv("ANR_HF_OCC");
+    const int o = e ? atoi(e) : 6;
+    return (o == 4 || o == 5 || o == 6) ? o : 6;
+  }();
+  return v;
+}
+template <int W, int NHD, bool BF, int OCC>
+static int launch_hf(const Args& a, const HashArgs& h, hipStream_t st) {
+  const void* fn = reinterpret_cast<const void*>(&hf_fwd_kernel<W, NHD, BF, HF_WAVES, OCC>);
+  static int pc = 0;
+  if (pc == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * HF_WAVES, 0) != hipSuccess || nb < 1) nb = 1;
+    pc = nb;
+  }
+  const int64_t n_super = (a.M + 63) / 64;
+  int64_t blocks = (n_super + HF_WAVES - 1) / HF_WAVES;
+  if (blocks > 256LL * pc) blocks = 256LL * pc;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((hf_fwd_kernel<W, NHD, BF, HF_WAVES, OCC>), dim3(blocks), dim3(64 * HF_WAVES),
+                     0, st, a, h);
+  return 0;
+}
+template <int W, int NHD, bool BF>
+static int run_hf(const Args& a, const HashArgs& h, hipStream_t st) {
+  switch (hf_occ()) {
+    case 4: return launch_hf<W, NHD, BF, 4>(a, h, st);
+    case 5: return launch_hf<W, NHD, BF, 5>(a, h, st);
+    default: return launch_hf<W, NHD, BF, 6>(a, h, st);
+  }
+}
+template <bool BF>
+static int dispatch_hf_t(int v, const Args& a, const HashArgs& h, hipStream_t st) {
+  switch (v) {
+    case 321: return run_hf<32, 1, BF>(a, h, st);
+    case 322: return run_hf<32, 2, BF>(a, h, st);
+    case 641: return run_hf<64, 1, BF>(a, h, st);
+    case 642: return run_hf<64, 2, BF>(a, h, st);
+  }
+  return 1;
+}
+
 template <bool BF>
 static int dispatch_t(int v, int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t st) {
   switch (v) {
@@ -1683,6 +1838,65 @@ static int field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
                          reinterpret_cast<hipStream_t>(stream)) == 0,
                 "anr_ingp_field_fwd: no kernel for this shape");
   ANR_CHECK_LAUNCH("anr_ingp_field_fwd");
+  return ANR_OK;
+}
+
+extern "C" int anr_ingp_hash_field_fwd(const anr_hashgrid_desc* grid, const float* x, int64_t M,
+                                      const void* table, int32_t table_dtype, void* planes,
+                                      int64_t plane_stride, const anr_mlp_desc* pos,
+                                      const anr_mlp_desc* dir, int32_t mma_dtype,
+                                      const void* packed, const float* dirs, int64_t n_per_ray,
+                                      float* sigma, float* color, int64_t color_stride,
+                                      anr_stream_t stream) {
+  const int v = variant(pos, dir);
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(grid && x && table && planes && packed && dirs && sigma && color,
+                "anr_ingp_hash_field_fwd: null pointer");
+  if (v == 0 || !mma_ok(mma_dtype) || table_dtype != ANR_F16 || grid->n_dims != 3 ||
+      grid->n_features != 2 || grid->n_levels != 16 || dir->n_output != 4 ||
+      n_per_ray < 64 || n_per_ray % 64 != 0 || color_stride < 4 || color_stride % 4 != 0) {
+    ::anr::set_error("anr_ingp_hash_field_fwd: unsupported configuration (3-D f16 grid of 16 "
+                     "levels x 2 features, a supported field pair with 4 colour outputs, "
+                     "samples per ray a multiple of 64, colour rows 16-byte aligned)");
+    return ANR_E_UNSUPPORTED;
+  }
+  ANR_CHECK_ARG(M > 0 && plane_stride >= 8 * M && plane_stride % 8 == 0,
+                "anr_ingp_hash_field_fwd: bad M / plane_stride (>= 8 M, multiple of 8)");
+  ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(planes) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(packed) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(color) & 15) == 0,
+                "anr_ingp_hash_field_fwd: planes / packed / color must be 16-byte aligned");
+  ::anr::GridLevels G;
+  ANR_CHECK_ARG(::anr::make_levels(grid, &G), "anr_ingp_hash_field_fwd: descriptor not initialised");
+  const int64_t lim = int64_t(1) << 31;
+  const int64_t t_bytes = static_cast<int64_t>(G.offset[15] + G.size[15]) * 4;
+  const int64_t o_bytes = (3 * plane_stride + 8 * M) * 2;
+  ANR_CHECK_ARG((M + 64) * 12 < lim && t_bytes < lim && o_bytes < lim && plane_stride * 2 < lim &&
+                    M * color_stride * 4 < lim,
+                "anr_ingp_hash_field_fwd: byte ranges must stay below 2^31");
+  Args a{};
+  a.packed = static_cast<const _Float16*>(packed);
+  a.dirs = dirs;
+  a.n_per_ray = static_cast<uint32_t>(n_per_ray);
+  a.M = M;
+  a.n_out = dir->n_output;
+  a.sigma = sigma;
+  a.color = color;
+  a.color_stride = color_stride;
+  HashArgs h{};
+  h.G = G;
+  h.x = x;
+  h.x_bytes = static_cast<uint32_t>(M * 12);
+  h.table = static_cast<const __half*>(table);
+  h.table_bytes = static_cast<uint32_t>(t_bytes);
+  h.planes = static_cast<_Float16*>(planes);
+  h.plane_bytes = static_cast<uint32_t>(plane_stride * 2);
+  h.out_bytes = static_cast<uint32_t>(o_bytes);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int rc = mma_dtype == ANR_BF16 ? dispatch_hf_t<true>(v, a, h, st)
+                                       : dispatch_hf_t<false>(v, a, h, st);
+  ANR_CHECK_ARG(rc == 0, "anr_ingp_hash_field_fwd: no kernel for this shape");
+  ANR_CHECK_LAUNCH("anr_ingp_hash_field_fwd");
   return ANR_OK;
 }
 

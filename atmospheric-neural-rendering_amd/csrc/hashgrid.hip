@@ -21,6 +21,7 @@
 // feature row (L*F values) is read/written contiguously.
 
 #include "anr_common.h"
+#include "hash_levels.h"
 
 // Profiling ablation (tools): 1 = backward without its atomics. 0 in product builds.
 #ifndef HASH_BS
@@ -43,81 +44,6 @@
 #include <cstdlib>
 
 namespace anr {
-
-struct GridLevels {
-  uint32_t offset[ANR_MAX_LEVELS];
-  uint32_t size[ANR_MAX_LEVELS];  // hashmap size T_l (entries)
-  uint32_t res[ANR_MAX_LEVELS];
-  float scale[ANR_MAX_LEVELS];
-};
-
-template <int D>
-__device__ __forceinline__ uint32_t grid_index(uint32_t T, uint32_t res, const uint32_t* g) {
-  uint32_t stride = 1, index = 0;
-#pragma unroll
-  for (int d = 0; d < D && stride <= T; ++d) {
-    index += g[d] * stride;
-    stride *= res;
-  }
-  if (T < stride) {
-    constexpr uint32_t primes[3] = {1u, 2654435761u, 805459861u};
-    index = 0;
-#pragma unroll
-    for (int d = 0; d < D; ++d) index ^= g[d] * primes[d];
-    // hashed levels have T = 2^log2_hashmap_size (checked by make_levels): % T == & (T-1)
-    return index & (T - 1u);
-  }
-  // dense levels: index < T except at the far faces (a corner at res) or for coordinates
-  // outside [0, 1]; the division is only paid there
-  return index < T ? index : index % T;
-}
-
-// Per-level corner indexing with the per-cell work hoisted: the 2^D corner indices of a
-// cell are built from 2 values per dimension (coordinate and coordinate+1, each times the
-// dense stride or the hash prime) with one 3-input add (dense) or xor (hashed) per
-// corner. Same result as grid_index for every corner, dense wrap (far faces, coordinates
-// outside [0,1]) included; branch-free apart from the rare full modulo.
-template <int D>
-struct LevelIdx {
-  uint32_t T, mul[D], res1;  // res1 = res - 1
-  bool hashed;
-  __device__ void init(uint32_t T_, uint32_t res) {
-    constexpr uint32_t primes[3] = {1u, 2654435761u, 805459861u};
-    T = T_;
-    res1 = res - 1u;
-    uint64_t st = 1;
-    uint32_t stride[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      stride[d] = static_cast<uint32_t>(st);
-      st *= res;
-    }
-    hashed = st > T;  // res^D > T, as grid_index decides
-#pragma unroll
-    for (int d = 0; d < D; ++d) mul[d] = hashed ? primes[d] : stride[d];
-  }
-  // comp[d][o] = (cell[d] + o) * mul[d]  (uint32 wrap, as tcnn)
-  __device__ void dims(const uint32_t* cell, uint32_t (*comp)[2]) const {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      comp[d][0] = cell[d] * mul[d];
-      comp[d][1] = comp[d][0] + mul[d];
-    }
-  }
-  // corner c: bit d = offset along dimension d
-  __device__ uint32_t corner(const uint32_t (*comp)[2], int c) const {
-    uint32_t hx = 0u, sum = 0u;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      hx ^= comp[d][(c >> d) & 1];
-      sum += comp[d][(c >> d) & 1];
-    }
-    if (hashed) return hx & (T - 1u);
-    if (sum < T) return sum;
-    const uint32_t s1 = sum - T;
-    return s1 < T ? s1 : sum % T;
-  }
-};
 
 // Corner addressing for the v2 walkers, where a lane owns the x-offset b and the NC =
 // 2^(D-1) corners over dims 1..D-1. The per-dimension components of the cell are formed
@@ -466,34 +392,6 @@ struct Corners {
 //     reads the f16 operand in place: no conversions).
 // Same corner order, weights and fma chain as v1: results are bit-identical to it. The
 // default forward since r02 (0.667 -> 0.648 ms at bench size).
-template <typename TT>
-struct Raw2;
-template <>
-struct Raw2<__half> {
-  using type = uint32_t;  // the two f16 features of one entry
-  static constexpr uint32_t bytes = 4;
-  __device__ static type load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
-  }
-  __device__ static void fma2(float wt, type v, float& a0, float& a1) {
-    const __half2 h = __builtin_bit_cast(__half2, v);
-    a0 = fmaf(wt, __low2float(h), a0);
-    a1 = fmaf(wt, __high2float(h), a1);
-  }
-};
-template <>
-struct Raw2<float> {
-  using type = uint32_t __attribute__((vector_size(8)));
-  static constexpr uint32_t bytes = 8;
-  __device__ static type load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
-  }
-  __device__ static void fma2(float wt, type v, float& a0, float& a1) {
-    a0 = fmaf(wt, __uint_as_float(v[0]), a0);
-    a1 = fmaf(wt, __uint_as_float(v[1]), a1);
-  }
-};
-
 template <typename TO>
 __device__ __forceinline__ void store2(__amdgpu_buffer_rsrc_t r, uint32_t off, float a0, float a1);
 template <>
@@ -508,12 +406,6 @@ __device__ __forceinline__ void store2<float>(__amdgpu_buffer_rsrc_t r, uint32_t
   using v2 = uint32_t __attribute__((vector_size(8)));
   const v2 v = {__float_as_uint(a0), __float_as_uint(a1)};
   __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, uint32_t bytes) {
-  // descriptor words provably wave-uniform (kernel arguments), so no waterfall loops
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, static_cast<int>(bytes),
-                                           0x00020000);
 }
 
 // One lane's walk of v6: level ``level`` over the K samples of the chunk starting at m0,
@@ -680,7 +572,6 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_planes_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, uint32_t x_bytes, uint32_t xs4,
     int64_t M, const TT* __restrict__ table, uint32_t table_bytes, __half* __restrict__ out,
     uint32_t out_bytes, uint32_t plane_bytes) {
-  using R = Raw2<TT>;
   const int64_t m = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   const __amdgpu_buffer_rsrc_t rx = wave_rsrc(x, x_bytes);
   const __amdgpu_buffer_rsrc_t rt = wave_rsrc(table, table_bytes);
@@ -702,65 +593,7 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_planes_kernel(
   const int n_quads = (n_levels + 3) >> 2;
   for (int q = 0; q < n_quads; ++q) {
     uint32_t packed[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int level = 4 * q + j;
-      packed[j] = 0u;  // a partial last quad is zero-filled
-      if (level >= n_levels) continue;  // wave-uniform
-      const float scale = G.scale[level];
-      const uint32_t res = G.res[level];
-      const uint32_t T = G.size[level];
-      const uint32_t base = G.offset[level] * R::bytes;
-      LevelIdx<D> li;
-      li.init(T, res);
-      const uint32_t hmask = T - 1u;
-      float w[D];
-      uint32_t g[D];
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const float p = fmaf(scale, xv[d], 0.5f);
-        const float fl = floorf(p);
-        g[d] = static_cast<uint32_t>(static_cast<int>(fl));
-        w[d] = p - fl;
-      }
-      uint32_t comp[D][2];
-      li.dims(g, comp);
-      uint32_t idx[1 << D], sum[1 << D];
-#pragma unroll
-      for (int c = 0; c < (1 << D); ++c) {
-        uint32_t hx = 0u, sm = 0u;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          hx ^= comp[d][(c >> d) & 1];
-          sm += comp[d][(c >> d) & 1];
-        }
-        sum[c] = sm;
-        idx[c] = li.hashed ? (hx & hmask) : sm;
-      }
-      uint32_t gmax = g[0];
-#pragma unroll
-      for (int d = 1; d < D; ++d) gmax = gmax > g[d] ? gmax : g[d];
-      if (!li.hashed && gmax >= res - 1u) {
-#pragma unroll
-        for (int c = 0; c < (1 << D); ++c)
-          if (sum[c] >= T) {
-            const uint32_t s1 = sum[c] - T;
-            idx[c] = s1 < T ? s1 : sum[c] % T;
-          }
-      }
-      typename R::type val[1 << D];
-#pragma unroll
-      for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, base + idx[c] * R::bytes);
-      float a0 = 0.0f, a1 = 0.0f;
-#pragma unroll
-      for (int c = 0; c < (1 << D); ++c) {
-        float wt = 1.0f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) wt *= ((c >> d) & 1) ? w[d] : 1.0f - w[d];
-        R::fma2(wt, val[c], a0, a1);
-      }
-      packed[j] = __builtin_bit_cast(uint32_t, __floats2half2_rn(a0, a1));
-    }
+    plane_quad<D, TT>(G, n_levels, q, xv, rt, packed);
     typedef uint32_t u4q __attribute__((vector_size(16)));
     const u4q v = {packed[0], packed[1], packed[2], packed[3]};
     __builtin_amdgcn_raw_buffer_store_b128(v, ro, static_cast<uint32_t>(q) * plane_bytes + orow,
@@ -1012,23 +845,6 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     // per lane (lanes above n_levels have returned; an instrument, not the hot path)
     if (n_req) atomicAdd(count, static_cast<unsigned long long>(n_req));
   }
-}
-
-static bool make_levels(const anr_hashgrid_desc* d, GridLevels* G) {
-  if (d->n_levels < 1 || d->n_levels > ANR_MAX_LEVELS) return false;
-  for (int l = 0; l < d->n_levels; ++l) {
-    G->offset[l] = d->offsets[l];
-    G->size[l] = d->offsets[l + 1] - d->offsets[l];
-    G->res[l] = d->resolutions[l];
-    G->scale[l] = d->scales[l];
-    if (G->size[l] == 0) return false;
-    // grid_index: a level too large for a dense table is hashed, and its size must be a
-    // power of two there (always true for tcnn's min(next_mult(res^D, 8), 2^log2T))
-    uint64_t dense = 1;
-    for (int k = 0; k < d->n_dims && dense <= G->size[l]; ++k) dense *= G->res[l];
-    if (dense > G->size[l] && (G->size[l] & (G->size[l] - 1)) != 0) return false;
-  }
-  return true;
 }
 
 // v2: one chunk per wave. Every chunk ends with a flush of all its held corners, so a

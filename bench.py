@@ -114,6 +114,11 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
                      "survey_bytes": M * (64 + 12 + 2 * grid.n_levels * 8 * 2 * 2)},
         # enc in, sigma + color out
         "field_fwd": {"bytes": M * (enc_b + 4 + 4 * nb), "flops": M * f_fwd},
+        # the two in one kernel (anr_ingp_hash_field_fwd, r06): coordinates in, f16
+        # features (planes, for the backward) + sigma + color out, the table once
+        "hash_field_fwd": {"bytes": M * (12 + enc_b + 4 + 4 * nb) + 2 * n_table,
+                           "flops": M * f_fwd,
+                           "survey_bytes": M * (12 + grid.n_levels * 8 * 2 * 2 + enc_b + 4 + 4 * nb)},
         # enc in, sigma out; the pos MLP only (extract / occupancy)
         "field_density": {"bytes": M * (enc_b + 4), "flops": M * mlp_flops(pos)},
         # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; dX + dW (2x the forward) is the
@@ -238,8 +243,10 @@ def target_rooflines(kernels: dict, mfma_key: str) -> dict:
     the hash-encode kernels' compulsory-byte HBM fraction (target >= 0.70) and the fused
     MLP kernels' MFMA fraction (target >= 0.50)."""
     out = {}
-    for name, key, tgt in (("hash_fwd", "hbm_frac", 0.70), ("hash_bwd", "hbm_frac", 0.70),
-                           ("field_fwd", "mfma_frac", 0.50), ("field_bwd", "mfma_frac", 0.50)):
+    for name, key, tgt in (("hash_fwd", "hbm_frac", 0.70), ("hash_field_fwd", "hbm_frac", 0.70),
+                           ("hash_bwd", "hbm_frac", 0.70), ("field_fwd", "mfma_frac", 0.50),
+                           ("hash_field_fwd", "mfma_frac", 0.50),
+                           ("field_bwd", "mfma_frac", 0.50)):
         k = kernels.get(name)
         if not k or key not in k:
             continue
@@ -251,7 +258,7 @@ def target_rooflines(kernels: dict, mfma_key: str) -> dict:
                   "hbm_frac_measured", "mfma_frac_measured"):
             if x in k:
                 e[x] = k[x]
-        out[name] = e
+        out[name if name != "hash_field_fwd" else f"hash_field_fwd:{key[:4]}"] = e
     return out
 
 

@@ -29,9 +29,10 @@
 extern "C" {
 #endif
 
-/* ABI 3 (r05): anr_hashgrid_fwd_planes, and the fused field entry points' enc_stride < 0
+/* ABI 4 (r06): anr_ingp_hash_field_fwd. ABI 3 (r05): anr_hashgrid_fwd_planes, and the fused
+ * field entry points' enc_stride < 0
  * selecting the level-quad-plane layout it writes. */
-#define ANR_ABI_VERSION 3
+#define ANR_ABI_VERSION 4
 
 enum anr_dtype { ANR_F32 = 0, ANR_F16 = 1, ANR_BF16 = 2 };
 
@@ -331,6 +332,20 @@ int anr_ingp_field_fwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t
                        const void* packed, const void* enc, int64_t enc_stride,
                        const float* dirs, int64_t n_per_ray, int64_t M, float* sigma,
                        float* color, int64_t color_stride, anr_stream_t stream);
+/* Hash-grid forward + field forward in one kernel (ABI 4, r06): the level-quad planes of
+ * anr_hashgrid_fwd_planes (written for the backward: planes, plane_stride >= 8 M f16
+ * elements) and sigma / color of anr_ingp_field_fwd, bit-identical to those two calls, with
+ * the planes never re-read. Replaces the same call sites (instant_ngp.py:163-171: the tcnn
+ * Encoding forward, pos_mlp, dir_encoder, dir_mlp). Shapes: 3-D f16 hash grid of 16 levels
+ * x 2 features (x: (M, 3) f32 rows), a supported field pair with 4 colour outputs, samples
+ * per ray a multiple of 64, 16-byte aligned planes / packed / colour rows;
+ * ANR_E_UNSUPPORTED otherwise (the two calls then serve). */
+int anr_ingp_hash_field_fwd(const anr_hashgrid_desc* grid, const float* x, int64_t M,
+                            const void* table, int32_t table_dtype, void* planes,
+                            int64_t plane_stride, const anr_mlp_desc* pos,
+                            const anr_mlp_desc* dir, int32_t mma_dtype, const void* packed,
+                            const float* dirs, int64_t n_per_ray, float* sigma, float* color,
+                            int64_t color_stride, anr_stream_t stream);
 /* Density only: sigma[r] = relu(pos_mlp(enc[r])[0]) (f32), bit-identical to
  * anr_ingp_field_fwd's sigma, without the dir MLP -- the extract loop
  * (scripts/extract.py:203-209 -> instant_ngp.py:208-247 reads only the extinction) and the

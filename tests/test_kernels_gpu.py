@@ -1320,3 +1320,65 @@ def test_hashgrid_bwd_tiles_equals_plain(dev, M):
     assert torch.isfinite(gb).all()
     assert (ga - gb).abs().max().item() <= 1e-5 * ga.abs().max().item()
     assert ((ga != 0) == (gb != 0)).float().mean().item() > 0.9999
+
+
+@pytest.mark.parametrize("mma", ["f16", "bf16"])
+@pytest.mark.parametrize("width,nhd", [(64, 2), (64, 1), (32, 2)])
+@pytest.mark.parametrize("R,n_per_ray", [(37, 64), (5, 1024), (8192, 1024)])
+def test_hash_field_fwd_equals_two_kernels(dev, mma, width, nhd, R, n_per_ray):
+    """anr_ingp_hash_field_fwd (r06: hash grid + field forward in one kernel) against
+    anr_hashgrid_fwd_planes followed by anr_ingp_field_fwd on the planes: the planes it
+    writes and sigma / colour are bit-identical, on ray-like coordinates (16 levels, T =
+    2^19, f16 table), for every supported field shape, f16 and bf16 MFMA, a ragged ray count
+    and the bench size (8,192 rays x 1,024 samples). Shapes outside its set (samples per ray
+    not a multiple of 64) are refused with ANR_E_UNSUPPORTED."""
+    from atmonr_amd import _lib
+
+    if R == 8192 and (width, nhd, mma) != (64, 2, "f16"):
+        pytest.skip("bench size: the bench's field only")
+    M, nb = R * n_per_ray, 4
+    code = _lib.BF16 if mma == "bf16" else _lib.F16
+    g = torch.Generator(device=dev).manual_seed(23)
+    lib = _lib.load()
+    d = _lib.hashgrid_desc(3, 16, 2, 16, 1.3819, 19)
+    o = torch.rand(R, 1, 3, device=dev, generator=g)
+    dr = (torch.rand(R, 1, 3, device=dev, generator=g) - 0.5) * 0.6
+    t = torch.linspace(0, 1, n_per_ray, device=dev)[None, :, None]
+    x = (o + dr * t).clamp(0, 1).reshape(M, 3).contiguous()
+    table = ((torch.rand(d.n_params, device=dev, generator=g) * 2 - 1) * 0.5).half()
+    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
+    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
+    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
+    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
+    dirs = torch.rand(R, 3, device=dev, generator=g)
+    s = _lib.stream(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", pb, db, code, pp.data_ptr(), pd.data_ptr(),
+              packed.data_ptr(), s)
+    out = {}
+    for name in ("two", "fused"):
+        planes = torch.full((4, M, 8), float("nan"), device=dev, dtype=torch.float16)
+        sigma = torch.full((M,), float("nan"), device=dev)
+        color = torch.full((M, nb), float("nan"), device=dev)
+        if name == "two":
+            _lib.call("anr_hashgrid_fwd_planes", ctypes.byref(d), x.data_ptr(), 3, M,
+                      table.data_ptr(), _lib.F16, planes.data_ptr(), 8 * M, s)
+            _lib.call("anr_ingp_field_fwd", pb, db, code, packed.data_ptr(), planes.data_ptr(),
+                      -8 * M, dirs.data_ptr(), n_per_ray, M, sigma.data_ptr(),
+                      color.data_ptr(), nb, s)
+        else:
+            _lib.call("anr_ingp_hash_field_fwd", ctypes.byref(d), x.data_ptr(), M,
+                      table.data_ptr(), _lib.F16, planes.data_ptr(), 8 * M, pb, db, code,
+                      packed.data_ptr(), dirs.data_ptr(), n_per_ray, sigma.data_ptr(),
+                      color.data_ptr(), nb, s)
+        torch.cuda.synchronize()
+        out[name] = (planes, sigma, color)
+    for a, b in zip(out["two"], out["fused"]):
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.float16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.float16 else b.view(torch.int32))
+    assert torch.isfinite(out["fused"][2]).all()
+    rc = lib.anr_ingp_hash_field_fwd(ctypes.byref(d), x.data_ptr(), M, table.data_ptr(),
+                                     _lib.F16, planes.data_ptr(), 8 * M, pb, db, code,
+                                     packed.data_ptr(), dirs.data_ptr(), 48, sigma.data_ptr(),
+                                     color.data_ptr(), nb, s)
+    assert rc == -3  # ANR_E_UNSUPPORTED: 48 samples per ray

@@ -278,7 +278,7 @@ def _hash_field_ok(grid, n_out: int, n_per_ray: int) -> bool:
 
 
 _ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"
-_HASH_FIELD = os.environ.get("ANR_HASH_FIELD", "1") != "0"
+_HASH_FIELD = os.environ.get("ANR_HASH_FIELD", "0") != "0"
 _TILE_SKIP = os.environ.get("ANR_TILE_SKIP", "0") != "0"
 
 

@@ -733,7 +733,7 @@ struct HashArgs {
   uint32_t out_bytes;    // bytes of the plane buffer (range check of the stores)
 };
 
-template <int W, int NHD, bool BF, int WAVES, int OCC>
+template <int W, int NHD, bool BF, int WAVES, int OCC, int DEDUP>
 __global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
 hf_fwd_kernel(Args a, HashArgs h) {
   using N = Net<W, NHD>;
@@ -764,7 +764,7 @@ hf_fwd_kernel(Args a, HashArgs h) {
 #pragma unroll 1
     for (int q = 0; q < 4; ++q) {
       uint32_t p[4];
-      plane_quad<3, __half>(h.G, 16, q, xv, rt, p);
+      plane_quad<3, __half, DEDUP>(h.G, 16, q, xv, rt, p);
       const u4q v = {p[0], p[1], p[2], p[3]};
       __builtin_amdgcn_raw_buffer_store_b128(v, ro, static_cast<uint32_t>(q) * h.plane_bytes + orow,
                                              0, 0);
@@ -1662,18 +1662,23 @@ static int variant(const anr_mlp_desc* pos, const anr_mlp_desc* dir) {
 // as fit on the chip at once (the occupancy query), each wavefront walking 64-sample
 // segments grid-stride
 constexpr int HF_WAVES = 8;
-// register cap (waves per SIMD) of the fused forward: ANR_HF_OCC = 4 / 5 / 6 (A/B hook)
+// register cap (waves per SIMD) of the fused forward, ANR_HF_OCC = 4 / 5 / 6, and its
+// run-leader gathers, ANR_HF_DEDUP = 0 / 1 (A/B hooks)
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 static int hf_occ() {
-  static const int v = [] {
-    const char* e = getenv("ANR_HF_OCC");
-    const int o = e ? atoi(e) : 6;
-    return (o == 4 || o == 5 || o == 6) ? o : 6;
-  }();
+  static const int v = env_int("ANR_HF_OCC", 6);
   return v;
 }
-template <int W, int NHD, bool BF, int OCC>
+static bool hf_dedup() {
+  static const bool v = env_int("ANR_HF_DEDUP", 0) != 0;
+  return v;
+}
+template <int W, int NHD, bool BF, int OCC, int DD>
 static int launch_hf(const Args& a, const HashArgs& h, hipStream_t st) {
-  const void* fn = reinterpret_cast<const void*>(&hf_fwd_kernel<W, NHD, BF, HF_WAVES, OCC>);
+  const void* fn = reinterpret_cast<const void*>(&hf_fwd_kernel<W, NHD, BF, HF_WAVES, OCC, DD>);
   static int pc = 0;
   if (pc == 0) {
     int nb = 0;
@@ -1684,17 +1689,21 @@ static int launch_hf(const Args& a, const HashArgs& h, hipStream_t st) {
   int64_t blocks = (n_super + HF_WAVES - 1) / HF_WAVES;
   if (blocks > 256LL * pc) blocks = 256LL * pc;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((hf_fwd_kernel<W, NHD, BF, HF_WAVES, OCC>), dim3(blocks), dim3(64 * HF_WAVES),
-                     0, st, a, h);
+  hipLaunchKernelGGL((hf_fwd_kernel<W, NHD, BF, HF_WAVES, OCC, DD>), dim3(blocks),
+                     dim3(64 * HF_WAVES), 0, st, a, h);
   return 0;
+}
+template <int W, int NHD, bool BF, int DD>
+static int run_hf_dd(const Args& a, const HashArgs& h, hipStream_t st) {
+  switch (hf_occ()) {
+    case 4: return launch_hf<W, NHD, BF, 4, DD>(a, h, st);
+    case 5: return launch_hf<W, NHD, BF, 5, DD>(a, h, st);
+    default: return launch_hf<W, NHD, BF, 6, DD>(a, h, st);
+  }
 }
 template <int W, int NHD, bool BF>
 static int run_hf(const Args& a, const HashArgs& h, hipStream_t st) {
-  switch (hf_occ()) {
-    case 4: return launch_hf<W, NHD, BF, 4>(a, h, st);
-    case 5: return launch_hf<W, NHD, BF, 5>(a, h, st);
-    default: return launch_hf<W, NHD, BF, 6>(a, h, st);
-  }
+  return hf_dedup() ? run_hf_dd<W, NHD, BF, HASH_DEDUP>(a, h, st) : run_hf_dd<W, NHD, BF, 0>(a, h, st);
 }
 template <bool BF>
 static int dispatch_hf_t(int v, const Args& a, const HashArgs& h, hipStream_t st) {

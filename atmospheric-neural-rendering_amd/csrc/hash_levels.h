@@ -5,6 +5,12 @@
 
 #include "anr_common.h"
 
+#ifndef HASH_DEDUP
+// plane_quad: levels whose cells change at no more than this many of a wavefront's lanes
+// gather at the run leaders only (see there); 0 = every lane gathers, 64 = every level
+#define HASH_DEDUP 64
+#endif
+
 namespace anr {
 
 struct GridLevels {
@@ -91,6 +97,10 @@ struct Raw2<__half> {
   __device__ static type load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
   }
+  // the value of lane src (ds_bpermute)
+  __device__ static type from_lane(type v, int src) {
+    return static_cast<type>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
+  }
   __device__ static void fma2(float wt, type v, float& a0, float& a1) {
     const __half2 h = __builtin_bit_cast(__half2, v);
     a0 = fmaf(wt, __low2float(h), a0);
@@ -103,6 +113,13 @@ struct Raw2<float> {
   static constexpr uint32_t bytes = 8;
   __device__ static type load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  }
+  __device__ static type from_lane(type v, int src) {
+    type o;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      o[k] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v[k])));
+    return o;
   }
   __device__ static void fma2(float wt, type v, float& a0, float& a1) {
     a0 = fmaf(wt, __uint_as_float(v[0]), a0);
@@ -121,7 +138,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, uint3
 // last quad is zero-filled) of the sample at coordinates xv: the forward v9 arithmetic
 // (one lane per sample, every corner gathered through the table descriptor rt; same corner
 // order, weights and fma chain as the walkers, bit-identical to them).
-template <int D, typename TT>
+template <int D, typename TT, int DEDUP = HASH_DEDUP>
 __device__ __forceinline__ void plane_quad(const GridLevels& G, int n_levels, int q,
                                            const float* xv, __amdgpu_buffer_rsrc_t rt,
                                            uint32_t (&packed)[4]) {
@@ -173,8 +190,42 @@ __device__ __forceinline__ void plane_quad(const GridLevels& G, int n_levels, in
         }
     }
     typename R::type val[1 << D];
+    bool plain = true;
+    if constexpr (DEDUP > 0) {
+      // Lanes are consecutive samples of a ray, so runs of lanes share a cell (one run per
+      // wavefront on the coarse levels, every few samples on the finest). The gathers'
+      // cost is address processing per active lane (profiles/r06_ta_probe.log: masked
+      // lanes are skipped), so only the first lane of each run gathers and the run's other
+      // lanes take its corner values through ds_bpermute (the LDS crossbar, not the
+      // texture path). Levels whose cells change at more than DEDUP lanes gather
+      // plainly. The same entries reach every lane: bit-identical.
+      const int lane = __lane_id();
+      bool lead = lane == 0;
 #pragma unroll
-    for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, base + idx[c] * R::bytes);
+      for (int d = 0; d < D; ++d) {
+        // the previous lane's cell (DPP wave_shr:1; lane 0 reads 0 and leads anyway)
+        const uint32_t pg = static_cast<uint32_t>(
+            __builtin_amdgcn_update_dpp(0, static_cast<int>(g[d]), 0x138, 0xf, 0xf, false));
+        lead = lead || pg != g[d];
+      }
+      const uint64_t lm = __ballot(lead);
+      if (__popcll(lm) <= DEDUP) {  // wave-uniform
+        plain = false;
+        // this lane's run leader: the highest leading lane at or below it
+        const uint64_t below = lm & ((2ull << lane) - 1ull);
+        const int src = 63 - static_cast<int>(__clzll(static_cast<long long>(below)));
+        if (lead) {
+#pragma unroll
+          for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, base + idx[c] * R::bytes);
+        }
+#pragma unroll
+        for (int c = 0; c < (1 << D); ++c) val[c] = R::from_lane(val[c], src);
+      }
+    }
+    if (plain) {
+#pragma unroll
+      for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, base + idx[c] * R::bytes);
+    }
     float a0 = 0.0f, a1 = 0.0f;
 #pragma unroll
     for (int c = 0; c < (1 << D); ++c) {

@@ -567,7 +567,7 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_v6_kernel(
 // on the bench coordinates (profiles/r05_hash_fwd_planes.log): v6 0.634 ms, v9 0.47-0.50
 // ms; pinning level pairs to XCDs (block b -> XCD b % 8) made it slower (0.77 / 1.13 ms:
 // every XCD then reads every coordinate).
-template <int D, typename TT>
+template <int D, typename TT, int DEDUP>
 __global__ void __launch_bounds__(256) hashgrid_fwd_planes_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, uint32_t x_bytes, uint32_t xs4,
     int64_t M, const TT* __restrict__ table, uint32_t table_bytes, __half* __restrict__ out,
@@ -593,7 +593,7 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_planes_kernel(
   const int n_quads = (n_levels + 3) >> 2;
   for (int q = 0; q < n_quads; ++q) {
     uint32_t packed[4];
-    plane_quad<D, TT>(G, n_levels, q, xv, rt, packed);
+    plane_quad<D, TT, DEDUP>(G, n_levels, q, xv, rt, packed);
     typedef uint32_t u4q __attribute__((vector_size(16)));
     const u4q v = {packed[0], packed[1], packed[2], packed[3]};
     __builtin_amdgcn_raw_buffer_store_b128(v, ro, static_cast<uint32_t>(q) * plane_bytes + orow,
@@ -860,6 +860,18 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
 static int64_t env_k(const char* name) {
   const char* e = getenv(name);  // profiling override of the chunk length
   return e ? atoll(e) : 0;
+}
+// run-leader gathers in the planes forward (plane_quad): ANR_HASH_DEDUP = the largest
+// number of cell changes per wavefront at which a level gathers at the run leaders only
+// (0 = off, 16 / 32 / 48 / 64; A/B hook, default HASH_DEDUP = 64: every level. Measured on
+// the settled bench step, hash fwd 0.478 ms off, 0.435 / 0.439 / 0.433 / 0.421 ms at
+// 32 / 16 / 48 / 64: profiles/r06_hash_fwd_dedup_sweep.log)
+static int plane_dedup() {
+  static const int v = [] {
+    const char* e = getenv("ANR_HASH_DEDUP");
+    return e ? atoi(e) : HASH_DEDUP;
+  }();
+  return v;
 }
 static int64_t pick_chunk_v2(int64_t M) {
   static const int64_t over = env_k("ANR_HASH_KB");
@@ -1212,8 +1224,19 @@ extern "C" int anr_hashgrid_fwd_planes(const anr_hashgrid_desc* d, const float* 
                     (M + 256) * x_stride * 4 < lim && plane_stride * 2 < lim,
                 "anr_hashgrid_fwd_planes: byte ranges must stay below 2^31");
   const dim3 grid(static_cast<unsigned>(ceil_div(M, 256))), block(256);
+  const int dd = plane_dedup();
 #define ANR_HG_PL(D_, TT)                                                                    \
-  hipLaunchKernelGGL((hashgrid_fwd_planes_kernel<D_, TT>), grid, block, 0, as_stream(stream), \
+  do {                                                                                       \
+    switch (dd) {                                                                            \
+      case 0: ANR_HG_PL1(D_, TT, 0); break;                                                  \
+      case 16: ANR_HG_PL1(D_, TT, 16); break;                                                \
+      case 48: ANR_HG_PL1(D_, TT, 48); break;                                                \
+      case 32: ANR_HG_PL1(D_, TT, 32); break;                                                \
+      default: ANR_HG_PL1(D_, TT, HASH_DEDUP); break;                                        \
+    }                                                                                        \
+  } while (0)
+#define ANR_HG_PL1(D_, TT, DD)                                                               \
+  hipLaunchKernelGGL((hashgrid_fwd_planes_kernel<D_, TT, DD>), grid, block, 0, as_stream(stream), \
                      G, d->n_levels, x, static_cast<uint32_t>(x_bytes),                      \
                      static_cast<uint32_t>(x_stride * 4), M, static_cast<const TT*>(table),  \
                      static_cast<uint32_t>(t_bytes), static_cast<__half*>(out),              \
@@ -1226,6 +1249,7 @@ extern "C" int anr_hashgrid_fwd_planes(const anr_hashgrid_desc* d, const float* 
     else ANR_HG_PL(2, float);
   }
 #undef ANR_HG_PL
+#undef ANR_HG_PL1
   ANR_CHECK_LAUNCH("anr_hashgrid_fwd_planes");
   return ANR_OK;
 }

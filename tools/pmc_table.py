@@ -16,6 +16,7 @@ import sys
 KERNELS = {"hash_fwd": "hashgrid_fwd_planes_kernel<",
            "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32",
            "field_fwd": "field::fwd_kernel<64, 2",
+           "hash_field_fwd": "hf_fwd_kernel<64, 2",
            "field_bwd": "field::bwd_rt_kernel<64, 2, true, false",
            "sampler": "sample_uniform_bins_kernel",
            "comp_fwd": "ref16::fwd_kernel<",

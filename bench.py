@@ -238,10 +238,12 @@ def _roof(mdl: dict, avg_ms: float, peaks: dict, mfma_key: str) -> dict:
     return r
 
 
-def target_rooflines(kernels: dict, mfma_key: str) -> dict:
+def target_rooflines(kernels: dict, mfma_key: str, pmc: dict | None = None,
+                     pmc_sfx: str = "") -> dict:
     """north_star's two kernel targets from the per-kernel table, against the spec peaks:
     the hash-encode kernels' compulsory-byte HBM fraction (target >= 0.70) and the fused
-    MLP kernels' MFMA fraction (target >= 0.50)."""
+    MLP kernels' MFMA fraction (target >= 0.50); with the rocprofv3 PMC bytes per launch of
+    the same kernel source (profiles/pmc_traffic.json) where they exist."""
     out = {}
     for name, key, tgt in (("hash_fwd", "hbm_frac", 0.70), ("hash_field_fwd", "hbm_frac", 0.70),
                            ("hash_bwd", "hbm_frac", 0.70), ("field_fwd", "mfma_frac", 0.50),
@@ -258,6 +260,11 @@ def target_rooflines(kernels: dict, mfma_key: str) -> dict:
                   "hbm_frac_measured", "mfma_frac_measured"):
             if x in k:
                 e[x] = k[x]
+        ent, stale = pmc_entry(pmc, name, pmc_sfx)
+        if ent and not stale:
+            e["traffic"] = ent["bytes"]
+            e["traffic_gbs"] = round(ent["bytes"] / (k["avg_ms"] * 1e-3) / 1e9, 1)
+            e["traffic_source"] = f"profiles/pmc_traffic.json [{ent.get('source')}]"
         out[name if name != "hash_field_fwd" else f"hash_field_fwd:{key[:4]}"] = e
     return out
 
@@ -1182,7 +1189,7 @@ def main():
                 "parallelism": f"dp{world}",
             },
             "roofline": roofline,
-            "roofline_targets": target_rooflines(kernels, mfma_key),
+            "roofline_targets": target_rooflines(kernels, mfma_key, pmc, pmc_sfx),
             "cpu_baseline": cpu,
             "strong_scaling": strong,
             "alt_numerics": alt,

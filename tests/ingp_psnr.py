@@ -46,8 +46,10 @@ def train_side_by_side(runners: dict, scene, n_samples: int, checkpoints=CHECKPO
     while True:
         if it in checkpoints:
             for k, r in runners.items():
+                # a runner with render_from > it skips this checkpoint's render (psnr None)
+                skip = it < getattr(r, "render_from", 0)
                 out[k].append({"iteration": it, "loss": loss[k],
-                               "psnr": render_psnr(r.render, scene, n_samples)})
+                               "psnr": None if skip else render_psnr(r.render, scene, n_samples)})
             if progress is not None:
                 progress(out)
         if it >= last:

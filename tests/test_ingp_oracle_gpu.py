@@ -386,6 +386,7 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
                                         p_ref.scale, scene.max_i, half=True,
                                         semantics="reference")
             runners[name] = OracleRunner(oa, OPT, perturb_dirs=dirs, master=master)
+            runners[name].render_from = horizon + 1  # the arms are compared past the horizon
             arms.append(name)
     key = "psnr_reference_semantics" + ("" if n_samples == N else f"_n{n_samples}")
     out = train_side_by_side(runners, scene, n_samples, checkpoints=checkpoints, batch=batch,
@@ -397,7 +398,7 @@ def test_psnr_vs_reference_semantics(scene, dev, n_samples, batch, checkpoints):
                "psnr_gpu_build": out["gpu_build"][i]["psnr"]}
         row["delta_reference_numerics_db"] = row["psnr_gpu_reference_numerics"] - r["psnr"]
         row["delta_build_db"] = row["psnr_gpu_build"] - r["psnr"]
-        if replicas:
+        if replicas and r["iteration"] > horizon:
             runs = [row["psnr_gpu_reference_numerics"]] + [out[k][i]["psnr"] for k in replicas]
             oracles = [out[k][i]["psnr"] for k in arms]
             row["psnr_gpu_replicas"] = runs

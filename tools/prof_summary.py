@@ -26,19 +26,24 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "atmospheric-neural-rendering_amd", "csrc")
 # bench.py kernel tag prefix -> the source file that defines it (PMC entries carry its
 # sha1, and bench.py ignores an entry whose kernel source has changed since)
-SOURCES = {"hash": "hashgrid.hip", "field": "field_fused.hip", "composite": "composite.hip",
-           "sampler": "sampler.hip"}
+SOURCES = {"hash": ("hashgrid.hip", "hash_levels.h"), "field": ("field_fused.hip", "hash_levels.h"),
+           "composite": ("composite.hip",), "sampler": ("sampler.hip",)}
 
 
 def source_sha1(tag: str) -> str | None:
-    f = SOURCES.get(tag.split("_")[0])
-    if f is None:
+    files = SOURCES.get(tag.split("_")[0])
+    if files is None:
         return None
-    return hashlib.sha1(open(os.path.join(CSRC, f), "rb").read()).hexdigest()
+    h = hashlib.sha1()
+    for f in files:
+        h.update(open(os.path.join(CSRC, f), "rb").read())
+    return h.hexdigest()
 
 # bench.py kernel tag -> substring of the mangled/demangled kernel name
 TAGS = {  # prefixes: one instantiation of each per bench run (width / dtype follow --variant, --dtype)
-    "hash_fwd": "hashgrid_fwd_v6_kernel<3,",
+    "hash_fwd": "hashgrid_fwd_planes_kernel<3, __half",
+    "hash_fwd_v6": "hashgrid_fwd_v6_kernel<3,",
+    "hash_field_fwd": "hf_fwd_kernel<64, 2",
     "hash_fwd_v1": "hashgrid_fwd_kernel<3,",
     "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32, false, 6>",
     "hash_bwd_rtstride": "hashgrid_bwd_v2_kernel<3, float, 0, 0>",

@@ -58,6 +58,14 @@ SPEC_PEAKS = {"hbm_copy_gbs": 8000.0, "mfma_f16_tfs": 2500.0, "mfma_bf16_tfs": 2
               "mfma_f32_tfs": 157.3, "atomic_seg16_greq_s": 20.3, "source": "spec"}
 
 
+_T0 = time.time()
+
+
+def say(msg: str) -> None:
+    """Progress on stderr (rank 0's JSON line stays the only stdout line)."""
+    print(f"[bench {time.time() - _T0:6.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def measured_peaks(dev, spec: bool) -> dict:
     if spec:
         return dict(SPEC_PEAKS)
@@ -860,6 +868,7 @@ def main():
     ds = SyntheticHARP2Dataset(n_views=args.views, img_size=args.img_size, device=dev, seed=0)
     torch.cuda.synchronize()
     t_scene = time.time() - t0
+    say(f"scene built ({t_scene:.1f} s)")
     if args.workload == "nerf":
         return run_nerf(args, ds, dev, rank, world, t_scene)
     if args.workload == "extract":
@@ -891,8 +900,10 @@ def main():
     pipe, bucket, opt = job.pipe, job.bucket, job.opt
     sharded = job.sharded
     step = job.step
+    say(f"job built ({numerics} numerics); warm start")
     warm = (None if args.cold_start else
             warm_start(job, args, cfg, ds, dev, rank, world, rank_batch, shard))
+    say("warm start done; settling")
     transient = None
     if warm is not None and args.settle > 0:
         # The reference numerics' state right after the build-numerics warm start is a
@@ -930,6 +941,7 @@ def main():
     # that kernel's launches (events around every call would cost ~0.2 ms per step). A
     # graphed job profiles its eager form (the same kernels and arguments).
     M = rank_batch * args.samples
+    say("warm-up done; measuring peaks")
     peaks = measured_peaks(dev, args.spec_peaks)
     mfma_key = {"f32": "mfma_f32_tfs", "bf16": "mfma_bf16_tfs"}.get(args.dtype, "mfma_f16_tfs")
     pmc = {}
@@ -1043,6 +1055,7 @@ def main():
         del step
         job.release()
         torch.cuda.empty_cache()
+        say(f"timed region done; the {other} numerics")
         ajob = IngpJob(args, cfg, ds, dev, rank, world, rank_batch, other, use_graph, shard,
                        None)
         awarm = warm_start(ajob, args, cfg, ds, dev, rank, world, rank_batch, shard)
@@ -1145,6 +1158,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline
 
+        say("CPU baseline (oracle, configs/nerf.json step)")
         cpu = cpu_baseline.run(budget_s=args.cpu_budget)
 
     if rank == 0:

@@ -12,6 +12,7 @@ reported, since threads beyond the quota only time-share.
 from __future__ import annotations
 
 import os
+import sys
 import time
 
 import torch
@@ -19,13 +20,20 @@ import torch
 
 def host_threads(threads: int | None = None) -> tuple[int, str]:
     """The host cores the job may run on (the box's own host cores): the
-    process's CPU affinity mask, else os.cpu_count()."""
+    process's CPU affinity mask (else os.cpu_count()), capped at the cgroup CPU quota when
+    one is set -- threads past the quota only time-share the same CPU time (on the GPU box
+    the mask lists 256 CPUs and the quota grants 16: 256 spinning OpenMP threads there
+    ran the step many times slower than 16)."""
     if threads is not None:
         return threads, "argument"
     try:
-        return len(os.sched_getaffinity(0)), "len(os.sched_getaffinity(0))"
+        n, src = len(os.sched_getaffinity(0)), "len(os.sched_getaffinity(0))"
     except (AttributeError, OSError):
-        return os.cpu_count() or 1, "os.cpu_count()"
+        n, src = os.cpu_count() or 1, "os.cpu_count()"
+    q = cpu_quota()
+    if q is not None and q < n:
+        return max(1, int(q + 0.999)), f"cgroup CPU quota ({src} = {n})"
+    return n, src
 
 
 def omp_share() -> int | None:
@@ -77,6 +85,12 @@ def _nerf_setup(seed: int):
     return ds, RefNeRFPipeline(prep, ds.scale)
 
 
+def _progress(msg: str, threads: int, t_start: float) -> None:
+    """One stderr line per CPU step (a long silent phase reads as a hang to a watchdog)."""
+    print(f"[cpu_baseline] {threads} threads, {msg} ({time.perf_counter() - t_start:.0f} s)",
+          file=sys.stderr, flush=True)
+
+
 def _time_steps(threads, batch_size, seed, warmup, timed, budget_s):
     ds, pipe = _nerf_setup(seed)
     torch.set_num_threads(threads)
@@ -88,12 +102,14 @@ def _time_steps(threads, batch_size, seed, warmup, timed, budget_s):
     t_start = time.perf_counter()
     for k in range(warmup):
         pipe.train_step(batch(k))
+        _progress(f"warm-up step {k + 1}/{warmup}", threads, t_start)
     times = []
     k = warmup
     while True:
         t0 = time.perf_counter()
         pipe.train_step(batch(k))
         times.append(time.perf_counter() - t0)
+        _progress(f"timed step {len(times)}/{timed}: {times[-1]:.2f} s", threads, t_start)
         k += 1
         if time.perf_counter() - t_start >= budget_s or len(times) >= timed:
             break

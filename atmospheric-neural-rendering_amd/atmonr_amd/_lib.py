@@ -180,6 +180,10 @@ _SIGNATURES = {
         c_int32,
         [POINTER(HashGridDesc), _P, c_int64, c_int64, _P, c_int32, c_int64, _P, _P, _P],
     ),
+    "anr_hashgrid_bwd_rows": (
+        c_int32,
+        [POINTER(HashGridDesc), _P, c_int64, c_int64, _P, c_int32, c_int64, _P, _P, _P],
+    ),
     "anr_hashgrid_force_v1": (c_int32, [c_int32]),
     "anr_hashgrid_bwd_chunk": (c_int64, [c_int64]),
     "anr_hashgrid_bwd_count_requests": (
@@ -305,6 +309,11 @@ _SIGNATURES = {
          c_int64, _P, c_int64, _P, _P, c_float, _P],
     ),
     "anr_ingp_field_bwd_ref16_tiles": (
+        c_int32,
+        [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
+         c_int64, _P, c_int64, _P, _P, c_float, _P, _P],
+    ),
+    "anr_ingp_field_bwd_ref16_rows": (
         c_int32,
         [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
          c_int64, _P, c_int64, _P, _P, c_float, _P, _P],

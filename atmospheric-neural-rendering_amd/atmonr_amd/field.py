@@ -199,12 +199,25 @@ class IngpFieldFn(torch.autograd.Function):
             d_color = torch.zeros(M, pipe.dir_mlp.n_output_dims, device=dev)
         d_color = d_color.float().contiguous()
         d_sigma = d_sigma.float().contiguous() if d_sigma is not None else None
-        d_enc = torch.empty(M, pipe.pos_encoder.hash_grids[0].n_out, device=dev, dtype=torch.float32)
+        n_enc = pipe.pos_encoder.hash_grids[0].n_out
         pdesc, ddesc = ctypes.byref(pipe.pos_mlp.desc), ctypes.byref(pipe.dir_mlp.desc)
         mma = _mma_code(pipe)
         ls = getattr(pipe, "loss_scale", None)
-        tiles = None
-        if ls:
+        tiles = row_nz = None
+        if ls and _ROW_BITS and not _TILE_SKIP and n_enc == 32 and ctx.rows is None:
+            # reference numerics (default since r06): dL/denc as f16 rows, the values
+            # tinycudann hands the hash grid (exactly f16 numbers), plus one bit per row with
+            # a nonzero value; the hash-grid backward loads and walks only those rows
+            # (~27 % of them once training settles). ANR_ROW_BITS=0: f32 rows, every row
+            # loaded, the per-sample zero test (the r05 form, A/B)
+            d_enc = torch.empty(M, n_enc, device=dev, dtype=torch.float16)
+            row_nz = torch.empty((M + 31) // 32, device=dev, dtype=torch.int32)
+            call("anr_ingp_field_bwd_ref16_rows", pdesc, ddesc, ptr(packed), ptr(enc),
+                 ctx.enc_ld, ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
+                 d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
+                 float(ls), ptr(row_nz), s, tag="field_bwd")
+        elif ls:
+            d_enc = torch.empty(M, n_enc, device=dev, dtype=torch.float32)
             # reference numerics: tcnn's loss-scaled f16 backward. ANR_TILE_SKIP=1: it also
             # marks the 32-row tiles whose incoming gradients are all zero and the hash-grid
             # backward skips them without loading. Off by default: measured no faster than
@@ -223,6 +236,7 @@ class IngpFieldFn(torch.autograd.Function):
                      d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
                      float(ls), s, tag="field_bwd")
         else:
+            d_enc = torch.empty(M, n_enc, device=dev, dtype=torch.float32)
             ws_bytes = _lib.load().anr_ingp_field_bwd_workspace_bytes(pdesc, ddesc, mma, M)
             ws = torch.empty(max(1, -(-ws_bytes // 4)), device=dev, dtype=torch.float32)
             if ctx.rows is None:
@@ -242,7 +256,11 @@ class IngpFieldFn(torch.autograd.Function):
             pipe._last_d_enc = d_enc
             pipe._last_hash_bwd = (coords, d_enc, g_hash)
             pipe._last_field_grads = (d_sigma, d_color)
-        if tiles is not None:
+        if row_nz is not None:
+            call("anr_hashgrid_bwd_rows", ctypes.byref(grid.desc), ptr(coords), 3, M,
+                 ptr(d_enc), _lib.F16, d_enc.stride(0), ptr(g_hash), ptr(row_nz), s,
+                 tag="hash_bwd")
+        elif tiles is not None:
             call("anr_hashgrid_bwd_tiles", ctypes.byref(grid.desc), ptr(coords), 3, M,
                  ptr(d_enc), _lib.F32, d_enc.stride(0), ptr(g_hash), ptr(tiles), s,
                  tag="hash_bwd")
@@ -280,6 +298,7 @@ def _hash_field_ok(grid, n_out: int, n_per_ray: int) -> bool:
 _ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"
 _HASH_FIELD = os.environ.get("ANR_HASH_FIELD", "0") != "0"
 _TILE_SKIP = os.environ.get("ANR_TILE_SKIP", "0") != "0"
+_ROW_BITS = os.environ.get("ANR_ROW_BITS", "1") != "0"
 
 
 def field_fused(pipe) -> bool:

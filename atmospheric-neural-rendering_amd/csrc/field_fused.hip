@@ -280,6 +280,10 @@ struct Args {
   // tile was walked), 0 if it was skipped (dL/denc rows zero) -- the hash-grid backward
   // then skips those rows without loading them (anr_hashgrid_bwd_tiles)
   uint8_t* tile_nz;
+  // anr_ingp_field_bwd_ref16_rows: dL/denc as f16 rows (instead of d_enc) and per 32-row
+  // tile a word of row bits, bit i set when row 32 t + i has a nonzero value
+  _Float16* d_enc_h;
+  uint32_t* row_nz;
 };
 
 // ROWS is a compile-time choice: a run-time test on a.rows in the prefetch paths put a
@@ -1028,10 +1032,14 @@ __device__ __forceinline__ h4 tr_b(h8 x, h8 sel) {
 // dir_encoder as f16(f16(g_scaled) / 128) (a subnormal-flushing f16 division) and is
 // rescaled for pos_mlp, and dL/denc is written as f16(f16(g_scaled) / 128)
 // (tinycudann/modules.py: input_grad / loss_scale, cast to the f16 input's dtype).
-template <int W, int NHD, bool FAST, bool ROWS, bool BF, bool REF = false>
+// REF 2 (anr_ingp_field_bwd_ref16_rows): the same arithmetic, dL/denc written as f16 (its
+// values are f16 numbers already, so the rows hold them exactly) plus one bit per row, set
+// when any of the row's 32 values is nonzero (a.row_nz, one 32-bit word per 32-row tile)
+template <int W, int NHD, bool FAST, bool ROWS, bool BF, int REF = 0>
 __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64_t tpw,
                                                      const float* wmax) {
   static_assert(!(REF && BF), "reference numerics are f16");
+  constexpr bool RMASK = REF == 2;
   // MT 16-sample halves per tile, the dW contraction over NP pairs of them. (64-sample
   // tiles, MT = 4, measured 6 % slower at the same 1 wave/SIMD: profiles/r03_field_bwd_ab.log)
   constexpr int MT = 2, TR = 16 * MT, NP = MT / 2;
@@ -1155,14 +1163,46 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) pend[kt][mt] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  // one lane's 4 values of dL/denc row `row`, columns 16 kt + 4 g .. + 3
+  auto put = [&](int64_t row, int kt, const f4& v) {
+    if constexpr (RMASK) {
+      const h4 hv = {static_cast<_Float16>(v[0]), static_cast<_Float16>(v[1]),
+                     static_cast<_Float16>(v[2]), static_cast<_Float16>(v[3])};
+      *reinterpret_cast<h4*>(a.d_enc_h + row * a.d_enc_stride + 16 * kt + 4 * g) = hv;
+    } else {
+      *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
+    }
+  };
+  // RMASK: the tile's row bits from each lane's "my 8 values of row (mt, li) are not all
+  // zero" (uniform control flow: the ballots need every lane); rows of a row's four lanes
+  // g = 0..3 sit at ballot bits li + 16 g
+  auto put_mask = [&](int64_t tile, const bool (&nz)[MT]) {
+    if constexpr (RMASK) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const uint64_t b = __ballot(nz[mt]);
+        const uint32_t r = static_cast<uint32_t>((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xFFFFull);
+        word |= r << (16 * mt);
+      }
+      if (lane == 0) a.row_nz[tile] = word;
+    }
+  };
+  auto nz_of = [](const f4& v0, const f4& v1) {
+    return v0[0] != 0.0f || v0[1] != 0.0f || v0[2] != 0.0f || v0[3] != 0.0f || v1[0] != 0.0f ||
+           v1[1] != 0.0f || v1[2] != 0.0f || v1[3] != 0.0f;
+  };
   auto store_pend = [&]() {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int64_t row = pend_tile * TR + mt * 16 + li;
-        *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = pend[kt][mt];
-      }
+      for (int mt = 0; mt < MT; ++mt) put(pend_tile * TR + mt * 16 + li, kt, pend[kt][mt]);
+    if constexpr (RMASK) {
+      bool nz[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) nz[mt] = nz_of(pend[0][mt], pend[1][mt]);
+      put_mask(pend_tile, nz);
+    }
   };
   auto process = [&](auto full_c, int64_t tile, RawRows(&nraw)[MT], RawRows(&nnext)[MT]) {
     constexpr bool FULL = decltype(full_c)::value;
@@ -1229,9 +1269,14 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
           const int64_t row = tile * TR + mt * 16 + li;
           if (full || row < a.M) {
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
-              *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = zero4;
+            for (int kt = 0; kt < 2; ++kt) put(row, kt, zero4);
           }
+        }
+        if constexpr (RMASK) {
+          bool nz[MT];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) nz[mt] = false;
+          put_mask(tile, nz);
         }
         return;
       }
@@ -1406,6 +1451,8 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
           mma32_acc_v<BF>(dP0[nt * 2 + 1], gp, x1);
         }
       }
+      // RMASK outside the pend path: the tile's rows, kept until both column halves are out
+      f4 keep[RMASK && !(FAST && FULL) ? 2 : 1][MT];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         f4 acc[MT], accs[MT];
@@ -1421,20 +1468,27 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int64_t row = tile * TR + mt * 16 + li;
-          if (full || row < a.M) {
-            f4 v = acc[mt] * inv_s;
-            if constexpr (REF) {
+          f4 v = acc[mt] * inv_s;
+          if constexpr (REF) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) v[i] = r16(r16(acc[mt][i]) * inv_s);
-            }
+            for (int i = 0; i < 4; ++i) v[i] = r16(r16(acc[mt][i]) * inv_s);
+          }
+          if constexpr (RMASK && !(FAST && FULL)) keep[kt][mt] = (full || row < a.M) ? v : z4;
+          if (full || row < a.M) {
             if constexpr (FAST && FULL)
               pend[kt][mt] = v;
             else
-              *reinterpret_cast<f4*>(a.d_enc + row * a.d_enc_stride + 16 * kt + 4 * g) = v;
+              put(row, kt, v);
           }
         }
       }
       if constexpr (FAST && FULL) pend_tile = tile;
+      if constexpr (RMASK && !(FAST && FULL)) {
+        bool nz[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) nz[mt] = nz_of(keep[0][mt], keep[1][mt]);
+        put_mask(tile, nz);
+      }
     }
     // the last dW MFMAs of the tile have written their accumulators before anything
     // (a loop-exit copy) reads them
@@ -1599,12 +1653,17 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
       if (a.rows) return 1;
       const BwdGeom gm = bwd_geom<W, NHD, BF>(a.M, fast);
       const dim3 grid(static_cast<unsigned>(gm.blocks)), block(64 * waves);
-      if (fast)
-        hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, true, false, false, true>), grid, block, 0, st, a,
-                           0.0f, gm.tpw, nullptr);
-      else
-        hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, false, false, false, true>), grid, block, 0, st,
-                           a, 0.0f, gm.tpw, nullptr);
+#define ANR_REF_BWD(FASTV, REFV)                                                             \
+  hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, FASTV, false, false, REFV>), grid, block, 0, st, a, \
+                     0.0f, gm.tpw, nullptr)
+      if (a.d_enc_h) {
+        if (fast) ANR_REF_BWD(true, 2);
+        else ANR_REF_BWD(false, 2);
+      } else {
+        if (fast) ANR_REF_BWD(true, 1);
+        else ANR_REF_BWD(false, 1);
+      }
+#undef ANR_REF_BWD
       return 0;
     }
   }
@@ -1915,7 +1974,8 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
                      const float* d_color, int64_t d_color_stride, float* d_enc,
                      int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
                      int64_t workspace_bytes, anr_stream_t stream, float loss_scale = 0.0f,
-                     uint8_t* tile_nz = nullptr) {
+                     uint8_t* tile_nz = nullptr, void* d_enc_h = nullptr,
+                     uint32_t* row_nz = nullptr) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_bwd: unsupported pos/dir MLP pair");
   ANR_CHECK_ARG(loss_scale == 0.0f || (loss_scale > 0.0f && mma_dtype == ANR_F16 && rows == nullptr),
@@ -1923,15 +1983,18 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   ANR_CHECK_ARG(mma_ok(mma_dtype), "anr_ingp_field_bwd: mma_dtype must be ANR_F16 or ANR_BF16");
   ANR_CHECK_ARG(M >= 0 && M < (1LL << 31), "anr_ingp_field_bwd: bad M");
   if (M == 0) return ANR_OK;
-  ANR_CHECK_ARG(packed && enc && dirs && d_color && d_enc && g_pos && g_dir,
+  ANR_CHECK_ARG(packed && enc && dirs && d_color && (d_enc || (d_enc_h && row_nz)) && g_pos && g_dir,
                 "anr_ingp_field_bwd: null pointer");
+  ANR_CHECK_ARG(d_enc_h == nullptr || loss_scale > 0.0f,
+                "anr_ingp_field_bwd: f16 rows and row bits are reference numerics only");
   ANR_CHECK_ARG(n_per_ray >= 1 && n_per_ray < (1LL << 31) && d_color_stride >= dir->n_output &&
                     d_enc_stride >= 32 && d_enc_stride % 4 == 0,
                 "anr_ingp_field_bwd: bad shape/stride");
   ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(enc) & 15) == 0 &&
                     (reinterpret_cast<uintptr_t>(packed) & 15) == 0 &&
-                    (reinterpret_cast<uintptr_t>(d_enc) & 15) == 0,
-                "anr_ingp_field_bwd: enc/packed/d_enc must be 16-byte aligned");
+                    (reinterpret_cast<uintptr_t>(d_enc) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(d_enc_h) & 7) == 0,
+                "anr_ingp_field_bwd: enc/packed/d_enc must be 16-byte aligned (f16 rows: 8)");
   Args a{};
   a.packed = static_cast<const _Float16*>(packed);
   ANR_CHECK_ARG(set_enc(a, enc, enc_stride, M),
@@ -1951,6 +2014,8 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   a.rows = rows;
   a.loss_scale = loss_scale;
   a.tile_nz = tile_nz;
+  a.d_enc_h = static_cast<_Float16*>(d_enc_h);
+  a.row_nz = row_nz;
   const int rc = dispatch(v, mma_dtype == ANR_BF16, 2, a, static_cast<float*>(workspace),
                           workspace_bytes, reinterpret_cast<hipStream_t>(stream));
   ANR_CHECK_ARG(rc != 2,
@@ -2034,6 +2099,22 @@ extern "C" int anr_ingp_field_bwd_ref16_tiles(const anr_mlp_desc* pos, const anr
   return field_bwd(pos, dir, ANR_F16, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
                    d_sigma, d_color, d_color_stride, d_enc, d_enc_stride, g_pos, g_dir, nullptr,
                    0, stream, loss_scale, tile_nz);
+}
+
+extern "C" int anr_ingp_field_bwd_ref16_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                             const void* packed, const void* enc,
+                                             int64_t enc_stride, const float* dirs,
+                                             int64_t n_per_ray, int64_t M, const float* d_sigma,
+                                             const float* d_color, int64_t d_color_stride,
+                                             void* d_enc_h, int64_t d_enc_stride, float* g_pos,
+                                             float* g_dir, float loss_scale, uint32_t* row_nz,
+                                             anr_stream_t stream) {
+  ANR_CHECK_ARG(loss_scale > 0.0f, "anr_ingp_field_bwd_ref16_rows: loss_scale must be > 0");
+  ANR_CHECK_ARG(d_enc_h != nullptr && row_nz != nullptr,
+                "anr_ingp_field_bwd_ref16_rows: null d_enc / row_nz");
+  return field_bwd(pos, dir, ANR_F16, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
+                   d_sigma, d_color, d_color_stride, nullptr, d_enc_stride, g_pos, g_dir, nullptr,
+                   0, stream, loss_scale, nullptr, d_enc_h, row_nz);
 }
 
 extern "C" int anr_ingp_field_fwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,

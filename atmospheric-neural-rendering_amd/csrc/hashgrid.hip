@@ -629,12 +629,16 @@ __device__ __forceinline__ uint32_t distinct_segments(bool active, uint64_t seg)
 // COUNT: the request-count instrument (anr_hashgrid_bwd_count_requests): the same walk,
 // but every flush instruction adds its number of distinct 64-B segments to *count
 // instead of issuing the atomics (dtable is not written)
-template <int D, typename TG, int XS, int DS, bool COUNT = false, int BSZ = HASH_BS>
+// SPARSE: anr_hashgrid_bwd_rows: row_nz holds one bit per dL/dy row (32 rows per word,
+// written by anr_ingp_field_bwd_ref16_rows), and only the rows whose bit is set are loaded
+// and walked (16 levels: every lane takes part in the chunk's compaction)
+template <int D, typename TG, int XS, int DS, bool COUNT = false, int BSZ = HASH_BS,
+          bool SPARSE = false>
 __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     GridLevels G, int n_levels, const float* __restrict__ x, int64_t x_stride_rt, int64_t M,
     int64_t K, const TG* __restrict__ dout, int64_t dout_stride_rt, float* __restrict__ dtable,
     int skip_zero, unsigned long long* __restrict__ count = nullptr,
-    const uint8_t* __restrict__ tile_nz = nullptr) {
+    const uint8_t* __restrict__ tile_nz = nullptr, const uint32_t* __restrict__ row_nz = nullptr) {
   constexpr int NC = Corners<D>::NC;
   const int64_t x_stride = XS > 0 ? XS : x_stride_rt;
   const int64_t dout_stride = DS > 0 ? DS : dout_stride_rt;
@@ -805,7 +809,57 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
       for (int d = 0; d < D; ++d) xb[j][d] = xn[j][d];
     }
   };
-  if (BSZ != 8 || tile_nz == nullptr) {  // the tile mask below is laid out for BS = 8
+  if constexpr (SPARSE) {
+    static_assert(XS == 3 && DS == 32 && !COUNT, "row-mask walk: fused-field layout only");
+    // The chunk's set rows, compacted in order into this wave's LDS slot (K <= 256, a
+    // multiple of 32; 64 rows per round: lane l tests row r0 + l), then walked in batches of
+    // BS with the next batch's coordinates (scalar loads) and gradients prefetched. Every
+    // loaded row is nonzero in some lane, so no per-sample test remains; the rows whose bit
+    // is clear are exactly those the dense walk's per-sample skip passes over, so the same
+    // corner sums reach the same entries.
+    __shared__ uint32_t sidx[4][256];
+    uint32_t* my = sidx[threadIdx.x >> 6];
+    typedef __attribute__((address_space(4))) const uint32_t cu32;
+    int n = 0;
+    for (int64_t r0 = m0; r0 < m1; r0 += 64) {
+      const cu32* mp = (const cu32*)(row_nz + (r0 >> 5));
+      const uint32_t lo = mp[0];
+      const uint32_t hi = r0 + 32 < m1 ? mp[1] : 0u;
+      uint64_t bits = (static_cast<uint64_t>(hi) << 32) | lo;
+      const int64_t span = m1 - r0;
+      if (span < 64) bits &= (1ull << span) - 1ull;
+      const int below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bits >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bits), 0u));
+      if ((bits >> lane) & 1ull) my[n + below] = static_cast<uint32_t>(r0 - m0 + lane);
+      n += __popcll(bits);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int BS = BSZ;
+    typedef __attribute__((address_space(4))) const float cf32;
+    auto load_rows = [&](int bb, float (*xo)[D], TG* go) {
+#pragma unroll
+      for (int j = 0; j < BS; ++j) {
+        const int k = bb + j < n ? bb + j : n - 1;  // past the end: the last row again (unused)
+        const int64_t m = m0 + __builtin_amdgcn_readfirstlane(static_cast<int>(my[k]));
+        const cf32* xp = (const cf32*)(x + m * 3);
+#pragma unroll
+        for (int d = 0; d < D; ++d) xo[j][d] = xp[d];
+        go[j] = dout[m * 32 + col];
+      }
+    };
+    if (n > 0) {
+      load_rows(0, xb, gb);
+      for (int bb = 0; bb < n; bb += BS) {
+        load_rows(bb + BS, xn, gn);
+#pragma unroll
+        for (int j = 0; j < BS; ++j)
+          if (bb + j < n) step(xb[j], to_f32<TG>(gb[j]));
+        advance();
+      }
+    }
+  } else if (BSZ != 8 || tile_nz == nullptr) {  // the tile mask below is laid out for BS = 8
     load_batch(m0, xb, gb);
     for (int64_t mb = m0; mb < m1; mb += BS) {
       load_batch(mb + BS, xn, gn);
@@ -1287,6 +1341,43 @@ extern "C" int anr_hashgrid_bwd_tiles(const anr_hashgrid_desc* d, const float* x
                        static_cast<const float*>(dout), dout_stride, dtable, bwd_skip_zero(),
                        nullptr, tile_nz);
   ANR_CHECK_LAUNCH("anr_hashgrid_bwd_tiles");
+  return ANR_OK;
+}
+
+extern "C" int anr_hashgrid_bwd_rows(const anr_hashgrid_desc* d, const float* x,
+                                     int64_t x_stride, int64_t M, const void* dout,
+                                     int32_t dout_dtype, int64_t dout_stride, float* dtable,
+                                     const uint32_t* row_nz, anr_stream_t stream) {
+  using namespace anr;
+  if (M == 0) return ANR_OK;
+  ANR_CHECK_ARG(d && x && dout && dtable && row_nz, "anr_hashgrid_bwd_rows: null argument");
+  ANR_CHECK_ARG(M > 0 && x_stride >= d->n_dims &&
+                    dout_stride >= (int64_t)d->n_levels * d->n_features,
+                "anr_hashgrid_bwd_rows: bad shape/stride");
+  ANR_CHECK_ARG(dout_dtype == ANR_F16 || dout_dtype == ANR_F32, "anr_hashgrid_bwd_rows: bad dtype");
+  GridLevels G;
+  ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_bwd_rows: descriptor not initialised");
+  const uint64_t grad_bytes =
+      (static_cast<uint64_t>(G.offset[d->n_levels - 1]) + G.size[d->n_levels - 1]) * 2u * 4u;
+  const int64_t K = pick_chunk_v2(M);
+  if (!(d->n_dims == 3 && d->n_features == 2 && d->n_levels == 16 && bwd_v2() &&
+        grad_bytes < 0x80000000ull && K % 32 == 0 && K <= 256 && x_stride == 3 &&
+        dout_stride == 32 && M < (int64_t{1} << 31))) {
+    // outside the row-mask walker's shapes: the rows are complete, the mask an optimisation
+    return anr_hashgrid_bwd(d, x, x_stride, M, dout, dout_dtype, dout_stride, dtable, stream);
+  }
+  const dim3 grid(static_cast<unsigned>(ceil_div(ceil_div(M, K), 4))), block(256);
+  if (dout_dtype == ANR_F16)
+    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, __half, 3, 32, false, HASH_BS, true>), grid,
+                       block, 0, as_stream(stream), G, d->n_levels, x, x_stride, M, K,
+                       static_cast<const __half*>(dout), dout_stride, dtable, 2, nullptr,
+                       nullptr, row_nz);
+  else
+    hipLaunchKernelGGL((hashgrid_bwd_v2_kernel<3, float, 3, 32, false, HASH_BS, true>), grid,
+                       block, 0, as_stream(stream), G, d->n_levels, x, x_stride, M, K,
+                       static_cast<const float*>(dout), dout_stride, dtable, 2, nullptr,
+                       nullptr, row_nz);
+  ANR_CHECK_LAUNCH("anr_hashgrid_bwd_rows");
   return ANR_OK;
 }
 

@@ -181,7 +181,8 @@ def count_hash_requests(job, n_samples: int) -> tuple[int, float, float] | None:
         pipe._keep_d_enc = False
     cnt = torch.zeros(1, dtype=torch.int64, device=coords.device)
     _lib.call("anr_hashgrid_bwd_count_requests", ctypes.byref(grid.desc), coords.data_ptr(),
-              3, coords.shape[0], d_enc.data_ptr(), _lib.F32, d_enc.stride(0),
+              3, coords.shape[0], d_enc.data_ptr(),
+              _lib.F16 if d_enc.dtype == torch.float16 else _lib.F32, d_enc.stride(0),
               g_hash.data_ptr(), cnt.data_ptr(), _lib.stream(coords.device))
     torch.cuda.synchronize()
     if os.environ.get("ANR_BENCH_DEBUG"):

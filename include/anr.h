@@ -32,7 +32,7 @@ extern "C" {
 /* ABI 4 (r06): anr_ingp_hash_field_fwd. ABI 3 (r05): anr_hashgrid_fwd_planes, and the fused
  * field entry points' enc_stride < 0
  * selecting the level-quad-plane layout it writes. */
-#define ANR_ABI_VERSION 4
+#define ANR_ABI_VERSION 5
 
 enum anr_dtype { ANR_F32 = 0, ANR_F16 = 1, ANR_BF16 = 2 };
 
@@ -189,6 +189,18 @@ int anr_hashgrid_bwd_count_requests(const anr_hashgrid_desc* d, const float* x,
 int anr_hashgrid_bwd_tiles(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
                            int64_t M, const void* dout, int32_t dout_dtype, int64_t dout_stride,
                            float* dtable, const uint8_t* tile_nz, anr_stream_t stream);
+
+/* anr_hashgrid_bwd with per-row bits (ABI 5): bit (m % 32) of row_nz[m / 32] set marks a
+ * row m of dout with a nonzero value (anr_ingp_field_bwd_ref16_rows writes them); the v2
+ * walker loads and walks only those rows. Rows whose bit is clear must be zero in dout
+ * (every row is still read when the shape is outside the walker). Same result as
+ * anr_hashgrid_bwd; shapes other than 3-D / 2 features / 16 levels / strides (3, 32) /
+ * chunks that are a multiple of 32 rows run anr_hashgrid_bwd on the complete rows.
+ * Replaces the same call site as anr_hashgrid_bwd (tcnn HashGrid backward,
+ * instant_ngp.py:163). */
+int anr_hashgrid_bwd_rows(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
+                          int64_t M, const void* dout, int32_t dout_dtype, int64_t dout_stride,
+                          float* dtable, const uint32_t* row_nz, anr_stream_t stream);
 
 /* Level-quad-plane forward (r05; hashgrid.hip forward v9, one lane per sample): the same
  * features as anr_hashgrid_fwd with f16 output, laid out as planes of four levels: level
@@ -591,6 +603,18 @@ int anr_ingp_field_bwd_ref16_tiles(const anr_mlp_desc* pos, const anr_mlp_desc* 
                                    int64_t d_color_stride, float* d_enc, int64_t d_enc_stride,
                                    float* g_pos, float* g_dir, float loss_scale,
                                    uint8_t* tile_nz, anr_stream_t stream);
+/* anr_ingp_field_bwd_ref16 writing dL/denc as f16 rows (d_enc_h: (M, >= 32) halves, row
+ * stride d_enc_stride, 8-byte aligned; the reference numerics' dL/denc values are f16
+ * numbers, tinycudann/modules.py casts them to the f16 input's dtype, so the rows hold them
+ * exactly) and one bit per row in row_nz (ceil(M / 32) words): bit (m % 32) of word m / 32
+ * set iff row m has a nonzero value. For anr_hashgrid_bwd_rows (ABI 5). */
+int anr_ingp_field_bwd_ref16_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
+                                  const void* packed, const void* enc, int64_t enc_stride,
+                                  const float* dirs, int64_t n_per_ray, int64_t M,
+                                  const float* d_sigma, const float* d_color,
+                                  int64_t d_color_stride, void* d_enc_h, int64_t d_enc_stride,
+                                  float* g_pos, float* g_dir, float loss_scale,
+                                  uint32_t* row_nz, anr_stream_t stream);
 /* anr_mlp_bwd_ws in f16 with tcnn's fixed loss scale: dL/dinput written as
  * f16(f16(g_scaled)/loss_scale). Specialised (fused) MLP shapes only. */
 int anr_mlp_bwd_ref16(const anr_mlp_desc* d, const void* params, const void* in,

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_struct_sizes():
     from atmonr_amd import _lib
 
-    assert _lib.load().anr_abi_version() == 4
+    assert _lib.load().anr_abi_version() == 5
     assert ctypes.sizeof(_lib.PrepParams) == 96
     assert ctypes.sizeof(_lib.MlpDesc) == 32
 

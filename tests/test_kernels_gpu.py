@@ -1322,6 +1322,121 @@ def test_hashgrid_bwd_tiles_equals_plain(dev, M):
     assert ((ga != 0) == (gb != 0)).float().mean().item() > 0.9999
 
 
+def _row_bits(d_enc):
+    """Row bits as anr_ingp_field_bwd_ref16_rows writes them: bit m % 32 of word m // 32
+    set iff row m has a nonzero value (int32 words)."""
+    nz = (d_enc != 0).any(1).to(torch.int64).cpu()
+    M = nz.numel()
+    nz = torch.nn.functional.pad(nz, (0, -M % 32)).view(-1, 32)
+    w = (nz << torch.arange(32, dtype=torch.int64)[None]).sum(1)
+    return torch.where(w >= 2**31, w - 2**32, w).to(torch.int32)
+
+
+@pytest.mark.parametrize("nb,n_per_ray,R", [(4, 64, 40), (4, 40, 13), (3, 64, 9), (4, 1024, 24)])
+def test_ingp_field_bwd_ref16_rows_equals_f32_rows(dev, nb, n_per_ray, R):
+    """anr_ingp_field_bwd_ref16_rows (r06, ABI 5) against anr_ingp_field_bwd_ref16 on the
+    same inputs: its f16 dL/denc rows hold exactly the f32 path's values (they are f16
+    numbers: f16(f16(g_scaled) / 128)), bit for bit; its row bits are exactly the rows with
+    a nonzero value; the parameter gradients agree up to the f32 atomic flush order. The
+    inputs mix rays whose incoming gradients are zero (skipped tiles), rows whose tiny
+    gradients underflow to zero dL/denc in f16, and ordinary rows; a ragged last tile
+    (M = 520) and the general (non-fast) d_color layout (3 outputs) are covered."""
+    from atmonr_amd import _lib
+
+    width, nhd = 64, 2
+    M = R * n_per_ray
+    g = torch.Generator(device=dev).manual_seed(11)
+    lib = _lib.load()
+    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
+    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
+    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
+    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
+    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
+    dirs = torch.rand(R, 3, device=dev, generator=g)
+    s = _lib.stream(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", pb, db, _lib.F16, pp.data_ptr(), pd.data_ptr(),
+              packed.data_ptr(), s)
+    dcol = (torch.randn(M, nb, device=dev, generator=g) * 1e-2).half().float()
+    dsig = (torch.randn(M, device=dev, generator=g) * 1e-3).half().float()
+    tiny = torch.rand(M, device=dev, generator=g) < 0.5
+    dcol[tiny] *= 1e-5
+    dsig[tiny] *= 1e-5
+    for r in range(0, R, 3):
+        dcol[r * n_per_ray:(r + 1) * n_per_ray] = 0.0
+        dsig[r * n_per_ray:(r + 1) * n_per_ray] = 0.0
+    outs = []
+    for rows in (False, True):
+        g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
+        if rows:
+            d_enc = torch.full((M, 32), float("nan"), device=dev, dtype=torch.float16)
+            bits = torch.full((-(-M // 32),), -7, device=dev, dtype=torch.int32)
+            _lib.call("anr_ingp_field_bwd_ref16_rows", pb, db, packed.data_ptr(), enc.data_ptr(),
+                      32, dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), 128.0,
+                      bits.data_ptr(), s)
+        else:
+            d_enc = torch.full((M, 32), float("nan"), device=dev)
+            bits = None
+            _lib.call("anr_ingp_field_bwd_ref16", pb, db, packed.data_ptr(), enc.data_ptr(), 32,
+                      dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), 128.0, s)
+        outs.append((d_enc, bits, g_pos, g_dir))
+    torch.cuda.synchronize()
+    (d32, _, gp32, gd32), (d16, bits, gp16, gd16) = outs
+    assert torch.equal(d16.float(), d32)
+    nzr = (d32 != 0).any(1).float().mean().item()
+    assert 0.05 < nzr < 0.95, nzr  # the mix above: both kinds of rows present
+    assert torch.equal(bits.cpu(), _row_bits(d32))
+    for a_, b_ in ((gp16, gp32), (gd16, gd32)):
+        assert (a_ - b_).abs().max().item() <= 2e-5 * b_.abs().max().item()
+
+
+@pytest.mark.parametrize("M", [262144, 1048576, 300000, 8192 * 1024])
+def test_hashgrid_bwd_rows_equals_plain(dev, M):
+    """anr_hashgrid_bwd_rows (r06, ABI 5) walks only the rows whose bit is set: with f16
+    dL/dy zero on ~70 % of the rows (in runs, as the settled reference numerics leave them)
+    and the bits of exactly the nonzero rows, the table gradient equals anr_hashgrid_bwd's
+    up to the f32 atomic order. Clearing the bits of some nonzero rows drops exactly those
+    rows (== the plain walker on dL/dy with them zeroed). M = 300,000 has chunks that are
+    not a multiple of 32 rows: the plain walker runs there on the complete rows."""
+    from atmonr_amd import _lib
+
+    cfg = (3, 16, 16, 1.3819, 19)
+    d = _lib.hashgrid_desc(*cfg[:1], cfg[1], 2, cfg[2], cfg[3], cfg[4])
+    x = _grid_inputs(dev, cfg, M, True).to(dev)
+    g = torch.Generator(device=dev).manual_seed(4)
+    dout = (torch.randn(M, 32, device=dev, generator=g) * 1e-3).half()
+    runs = torch.rand(-(-M // 8), device=dev, generator=g) < 0.5
+    zero = (runs.repeat_interleave(8)[:M]) | (torch.rand(M, device=dev, generator=g) < 0.4)
+    dout[zero] = 0.0
+    s = _lib.stream(dev)
+
+    def walk(name, dy, bits=None):
+        gt = torch.zeros(d.n_params, device=dev)
+        args = [ctypes.byref(d), x.data_ptr(), 3, M, dy.data_ptr(), _lib.F16, 32, gt.data_ptr()]
+        if bits is not None:
+            args.append(bits.to(dev).data_ptr())
+        _lib.call(name, *args, s)
+        torch.cuda.synchronize()
+        return gt
+
+    ga = walk("anr_hashgrid_bwd", dout)
+    gb = walk("anr_hashgrid_bwd_rows", dout, _row_bits(dout))
+    assert torch.isfinite(gb).all()
+    assert (ga - gb).abs().max().item() <= 1e-5 * ga.abs().max().item()
+    assert ((ga != 0) == (gb != 0)).float().mean().item() > 0.9999
+    if M == 300000:
+        return
+    drop = (~zero) & (torch.rand(M, device=dev, generator=g) < 0.2)
+    dz = dout.clone()
+    dz[drop] = 0.0
+    gc = walk("anr_hashgrid_bwd_rows", dout, _row_bits(dz))
+    gd = walk("anr_hashgrid_bwd", dz)
+    assert (gc - gd).abs().max().item() <= 1e-5 * gd.abs().max().item()
+    assert (gc - ga).abs().max().item() > 1e-3 * ga.abs().max().item()
+
+
 @pytest.mark.parametrize("mma", ["f16", "bf16"])
 @pytest.mark.parametrize("width,nhd", [(64, 2), (64, 1), (32, 2)])
 @pytest.mark.parametrize("R,n_per_ray", [(37, 64), (5, 1024), (8192, 1024)])

@@ -433,12 +433,14 @@ template <int W, int NHD>
 struct FwdWeights {
   using N = Net<W, NHD>;
   h8 p0[N::NT], p1[N::KB], d0[N::NT], d1[NHD == 2 ? N::NT * N::KB : 1], d2[N::KB];
-  __device__ void load(const _Float16* pk, int lane) {
+  // dir = false: the pos network's fragments only (tile_forward without the dir network)
+  __device__ void load(const _Float16* pk, int lane, bool dir = true) {
     auto ld = [&](int off) { return *reinterpret_cast<const h8*>(pk + off + lane * 8); };
 #pragma unroll
     for (int i = 0; i < N::NT; ++i) p0[i] = ld(N::oFP0 + i * N::F32);
 #pragma unroll
     for (int i = 0; i < N::KB; ++i) p1[i] = ld(N::oFP1 + i * N::F32);
+    if (!dir) return;
 #pragma unroll
     for (int i = 0; i < N::NT; ++i) d0[i] = ld(N::oFD0 + i * N::F32);
     if constexpr (NHD == 2) {
@@ -489,9 +491,12 @@ struct NoSink {
 
 // sink: receives every layer input as soon as it is computed (the backward writes them
 // to LDS there, so they need not stay live in registers)
+// dir = false (wave-uniform): the pos network only; col = 0 (the backward of a tile whose
+// dL/dcolor is zero in every row needs nothing of the dir network)
 template <int W, int NHD, int NM, bool BF, typename WS, typename SK>
 __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const bool* valid,
-                                             int g, Tile<W, NHD>* t, const SK& sink) {
+                                             int g, Tile<W, NHD>* t, const SK& sink,
+                                             bool dir = true) {
   using N = Net<W, NHD>;
   const f4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -515,6 +520,11 @@ __device__ __forceinline__ void tile_forward(const WS& fw, const Rows* in, const
     const h8 w = fw.P1(kb);
 #pragma unroll
     for (int mt = 0; mt < NM; ++mt) t[mt].po = mma32<BF>(w, cat(t[mt].hp[2 * kb], t[mt].hp[2 * kb + 1]), t[mt].po);
+  }
+  if (!dir) {
+#pragma unroll
+    for (int mt = 0; mt < NM; ++mt) t[mt].col = z4;
+    return;
   }
 #pragma unroll
   for (int mt = 0; mt < NM; ++mt) {
@@ -1281,6 +1291,25 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         return;
       }
     }
+    // A tile whose dL/dcolor is zero in every row (reference numerics: every tile once
+    // training settles -- tcnn's f16 composite backward rounds the per-sample colour
+    // gradients of the atmosphere's tiny weights to zero, profiles/r05_hash_bwd_state_tiles
+    // .log): the dir network's backward adds exactly 0 to its dW and returns dX = 0, so
+    // neither it nor the dir half of the forward recompute runs (wave-uniform); dL/dpos_out
+    // is then dL/dsigma alone. Exact for finite weights and activations (0 * x = 0).
+    // Reference numerics, fast d_color layout only: the build numerics' f32 colour
+    // gradients are never all zero, and the branch costs their kernel registers (spills);
+    // in the general-layout kernel the branch's register copies read dW accumulators right
+    // behind their inline-asm MFMAs (tools/mfma_hazards.py)
+    bool dir_walk = true;
+    if constexpr (REF && FAST) {
+      bool cnz = false;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        cnz = cnz || cur[mt].dc[0] != 0.0f || cur[mt].dc[1] != 0.0f || cur[mt].dc[2] != 0.0f ||
+              cur[mt].dc[3] != 0.0f;
+      dir_walk = __any(cnz);
+    }
     // ---- forward recompute of both 16-sample halves; every activation stays in registers
     Tile<W, NHD> t[MT];
     h4 gc[MT];
@@ -1290,8 +1319,8 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) valid[mt] = full || tile * TR + mt * 16 + li < a.M;
       FwdWeights<W, NHD> fwl;
-      fwl.load(wbt, lane);
-      tile_forward<W, NHD, MT, BF>(fwl, cur, valid, g, t, NoSink{});
+      fwl.load(wbt, lane, dir_walk);
+      tile_forward<W, NHD, MT, BF>(fwl, cur, valid, g, t, NoSink{}, dir_walk);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         dens[mt] = (REF ? r16(t[mt].po[0]) : t[mt].po[0]) > 0.0f;
@@ -1302,112 +1331,121 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
         gc[mt] = to_h4<BF>(gv);
       }
     }
-    auto last = [&](int mt, int kt) -> h4 { return NHD == 2 ? t[mt].hd1[kt] : t[mt].hd0[kt]; };
-    // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
-    // Each layer's W^T fragments are read from LDS at the start of the layer and pinned
-    // there (sched_barrier): the dW half of the layer, which needs no weights, then covers
-    // the LDS latency that a read placed at its use exposes (1 wave/SIMD).
-    h4 dl[MT][NT];
-    {
-      h4 wd2[NT];
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) wd2[kt] = bfrag16(N::oBD2 + kt * N::F16);
-      __builtin_amdgcn_sched_barrier(0);
-      h8 ga[NP];
-#pragma unroll
-      for (int pr = 0; pr < NP; ++pr)
-        ga[pr] = cat(trc(R0 + 0, gc[2 * pr]), trc(R0 + 1, gc[2 * pr + 1]));
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
-#pragma unroll
-        for (int pr = 0; pr < NP; ++pr) {
-          const h8 xl = cat(trc(R0 + 2 + 2 * kt, last(2 * pr, kt)), trc(R0 + 3 + 2 * kt, last(2 * pr + 1, kt)));
-          mma32_acc_v<BF>(dD2[kt], ga[pr], xl);
-        }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) dl[mt][kt] = mask_h4<BF>(dx16(wd2[kt], gc[mt]), last(mt, kt));
-      }
-    }
-    // ---- dir hidden layer 1 (NHD == 2): dW_D1 (W x W) += dl^T · X_d0 ; dh0 = D1^T dl
-    h4 dh0[MT][NT];
-    if constexpr (NHD == 2) {
-      h8 wd1[NT * KB];
-#pragma unroll
-      for (int i = 0; i < NT * KB; ++i) wd1[i] = bfrag32(N::oBD1 + i * N::F32);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int pr = 0; pr < NP; ++pr) {
-        h8 gb[NT];
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          gb[nt] = cat(trc(R1 + 2 * nt, dl[2 * pr][nt]), trc(R1 + 1 + 2 * nt, dl[2 * pr + 1][nt]));
-#pragma unroll
+    h4 dpo[MT];
+    if (dir_walk) {
+      auto last = [&](int mt, int kt) -> h4 { return NHD == 2 ? t[mt].hd1[kt] : t[mt].hd0[kt]; };
+      // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
+      // Each layer's W^T fragments are read from LDS at the start of the layer and pinned
+      // there (sched_barrier): the dW half of the layer, which needs no weights, then covers
+      // the LDS latency that a read placed at its use exposes (1 wave/SIMD).
+      h4 dl[MT][NT];
+      {
+        h4 wd2[NT];
+  #pragma unroll
+        for (int kt = 0; kt < NT; ++kt) wd2[kt] = bfrag16(N::oBD2 + kt * N::F16);
+        __builtin_amdgcn_sched_barrier(0);
+        h8 ga[NP];
+  #pragma unroll
+        for (int pr = 0; pr < NP; ++pr)
+          ga[pr] = cat(trc(R0 + 0, gc[2 * pr]), trc(R0 + 1, gc[2 * pr + 1]));
+  #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
-          const h8 xb = cat(trc(R1 + 8 + 2 * kt, t[2 * pr].hd0[kt]), trc(R1 + 9 + 2 * kt, t[2 * pr + 1].hd0[kt]));
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) mma32_acc_v<BF>(dD1[nt * NT + kt], gb[nt], xb);
+  #pragma unroll
+          for (int pr = 0; pr < NP; ++pr) {
+            const h8 xl = cat(trc(R0 + 2 + 2 * kt, last(2 * pr, kt)), trc(R0 + 3 + 2 * kt, last(2 * pr + 1, kt)));
+            mma32_acc_v<BF>(dD2[kt], ga[pr], xl);
+          }
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt) dl[mt][kt] = mask_h4<BF>(dx16(wd2[kt], gc[mt]), last(mt, kt));
         }
       }
-#pragma unroll
-      for (int kt = 0; kt < NT; ++kt) {
+      // ---- dir hidden layer 1 (NHD == 2): dW_D1 (W x W) += dl^T · X_d0 ; dh0 = D1^T dl
+      h4 dh0[MT][NT];
+      if constexpr (NHD == 2) {
+        h8 wd1[NT * KB];
+  #pragma unroll
+        for (int i = 0; i < NT * KB; ++i) wd1[i] = bfrag32(N::oBD1 + i * N::F32);
+        __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+        for (int pr = 0; pr < NP; ++pr) {
+          h8 gb[NT];
+  #pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            gb[nt] = cat(trc(R1 + 2 * nt, dl[2 * pr][nt]), trc(R1 + 1 + 2 * nt, dl[2 * pr + 1][nt]));
+  #pragma unroll
+          for (int kt = 0; kt < NT; ++kt) {
+            const h8 xb = cat(trc(R1 + 8 + 2 * kt, t[2 * pr].hd0[kt]), trc(R1 + 9 + 2 * kt, t[2 * pr + 1].hd0[kt]));
+  #pragma unroll
+            for (int nt = 0; nt < NT; ++nt) mma32_acc_v<BF>(dD1[nt * NT + kt], gb[nt], xb);
+          }
+        }
+  #pragma unroll
+        for (int kt = 0; kt < NT; ++kt) {
+          f4 acc[MT], accs[MT];
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = accs[mt] = z4;
+  #pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+  #pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+              dx32(wd1[kt * KB + kb], dl[mt][2 * kb], dl[mt][2 * kb + 1], acc[mt], accs[mt]);
+          }
+          dx_join(acc, accs);
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt) dh0[mt][kt] = mask_h4<BF>(acc[mt], t[mt].hd0[kt]);
+        }
+      } else {
+  #pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+          for (int kt = 0; kt < NT; ++kt) dh0[mt][kt] = dl[mt][kt];
+      }
+      // ---- dir input layer: dW_D0 (W x 32, k' order) += dh0^T · X_de ; dpos = D0^T dh0
+      {
+        h8 wd0[KB];
+  #pragma unroll
+        for (int kb = 0; kb < KB; ++kb) wd0[kb] = bfrag32(N::oBD0 + kb * N::F32);
+        __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+        for (int pr = 0; pr < NP; ++pr) {
+          h4 a0, a1, b0, b1;
+          trb(R0 + 0, t[2 * pr].xd, a0, a1);
+          trb(R0 + 2, t[2 * pr + 1].xd, b0, b1);
+          const h8 x0 = cat(a0, b0), x1 = cat(a1, b1);
+  #pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {
+            const h8 gd = cat(trc(R0 + 4 + 2 * nt, dh0[2 * pr][nt]), trc(R0 + 5 + 2 * nt, dh0[2 * pr + 1][nt]));
+            mma32_acc_v<BF>(dD0[nt * 2], gd, x0);
+            mma32_acc_v<BF>(dD0[nt * 2 + 1], gd, x1);
+          }
+        }
         f4 acc[MT], accs[MT];
-#pragma unroll
+  #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[mt] = accs[mt] = z4;
-#pragma unroll
+  #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            dx32(wd1[kt * KB + kb], dl[mt][2 * kb], dl[mt][2 * kb + 1], acc[mt], accs[mt]);
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt) dx32(wd0[kb], dh0[mt][2 * kb], dh0[mt][2 * kb + 1], acc[mt], accs[mt]);
         }
         dx_join(acc, accs);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) dh0[mt][kt] = mask_h4<BF>(acc[mt], t[mt].hd0[kt]);
+  #pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          if constexpr (REF) {
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) acc[mt][i] = r16(r16(r16(acc[mt][i]) * inv_s) * s);
+          }
+          // pos_out[:, 0] is the density: its gradient is dL/dsigma through the ReLU
+          const float dsv = dens[mt] ? cur[mt].ds * s : 0.0f;
+          acc[mt][0] = g == 0 ? dsv : acc[mt][0];
+          dpo[mt] = to_h4<BF>(acc[mt]);
+        }
       }
     } else {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int kt = 0; kt < NT; ++kt) dh0[mt][kt] = dl[mt][kt];
-    }
-    // ---- dir input layer: dW_D0 (W x 32, k' order) += dh0^T · X_de ; dpos = D0^T dh0
-    h4 dpo[MT];
-    {
-      h8 wd0[KB];
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) wd0[kb] = bfrag32(N::oBD0 + kb * N::F32);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int pr = 0; pr < NP; ++pr) {
-        h4 a0, a1, b0, b1;
-        trb(R0 + 0, t[2 * pr].xd, a0, a1);
-        trb(R0 + 2, t[2 * pr + 1].xd, b0, b1);
-        const h8 x0 = cat(a0, b0), x1 = cat(a1, b1);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          const h8 gd = cat(trc(R0 + 4 + 2 * nt, dh0[2 * pr][nt]), trc(R0 + 5 + 2 * nt, dh0[2 * pr + 1][nt]));
-          mma32_acc_v<BF>(dD0[nt * 2], gd, x0);
-          mma32_acc_v<BF>(dD0[nt * 2 + 1], gd, x1);
-        }
-      }
-      f4 acc[MT], accs[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = accs[mt] = z4;
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) dx32(wd0[kb], dh0[mt][2 * kb], dh0[mt][2 * kb + 1], acc[mt], accs[mt]);
-      }
-      dx_join(acc, accs);
-#pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        if constexpr (REF) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[mt][i] = r16(r16(r16(acc[mt][i]) * inv_s) * s);
-        }
-        // pos_out[:, 0] is the density: its gradient is dL/dsigma through the ReLU
-        const float dsv = dens[mt] ? cur[mt].ds * s : 0.0f;
-        acc[mt][0] = g == 0 ? dsv : acc[mt][0];
-        dpo[mt] = to_h4<BF>(acc[mt]);
+        f4 acc = z4;
+        acc[0] = g == 0 && dens[mt] ? cur[mt].ds * s : 0.0f;
+        dpo[mt] = to_h4<BF>(acc);
       }
     }
     // ---- pos output layer: dW_P1 (16 x W) += dpo^T · X_ph ; dhp = P1^T dpo

@@ -93,8 +93,10 @@ struct LaneCorners {
   // A corner with offset o along a dim keeps its lattice point in the new cell iff
   // n = o + (old - new) is 0 or 1; it then becomes corner n there.
   __device__ static bool leaves(int c, const int* dl) {
+    // bitwise, not short-circuit: || became a divergent branch (exec save / restore) per
+    // corner in the walk's flush
     bool out = static_cast<unsigned>((c & 1) + dl[1]) > 1u;
-    if constexpr (D == 3) out = out || static_cast<unsigned>((c >> 1) + dl[2]) > 1u;
+    if constexpr (D == 3) out = out | (static_cast<unsigned>((c >> 1) + dl[2]) > 1u);
     return out;
   }
   // Carry accumulators onto the new cell's corners, one dimension at a time with
@@ -221,7 +223,7 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_kernel(
       const float fl = floorf(p);
       g[d] = static_cast<uint32_t>(static_cast<int>(fl));
       w[d] = p - fl;
-      same = same && (g[d] == cell[d]);
+      same = same & (g[d] == cell[d]);
     }
     if (!same) {
       have = true;
@@ -335,7 +337,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_kernel(
       const float fl = floorf(p);
       g[d] = static_cast<uint32_t>(static_cast<int>(fl));
       w[d] = p - fl;
-      same = same && (g[d] == cell[d]);
+      same = same & (g[d] == cell[d]);
     }
     if (!same) {
       if (have) flush();
@@ -444,7 +446,7 @@ __device__ __forceinline__ void fwd_walk_v6(const GridLevels& G, int level, int6
       const float fl = floorf(p);
       g[d] = static_cast<uint32_t>(static_cast<int>(fl));
       w[d] = p - fl;
-      same = same && (g[d] == cell[d]);
+      same = same & (g[d] == cell[d]);
     }
     if (!same) {
       uint32_t comp[D][2];
@@ -693,7 +695,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
       const float fl = floorf(p);
       g[d] = static_cast<uint32_t>(static_cast<int>(fl));
       w[d] = p - fl;
-      same = same && (g[d] == cell[d]);
+      same = same & (g[d] == cell[d]);
     }
     if (!same) {
       if (have) {
@@ -711,8 +713,8 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
           // skip_zero: a leaving corner whose sum is exactly zero issues no request
           // (reference numerics: tcnn's x128 f16 backward rounds most dL/denc to zero);
           // without skip_zero only the leaving test applies
-          const bool out = (!keepx || LaneCorners<D>::leaves(c, dl)) &&
-                           (!skip_zero || acc[c] != 0.0f);
+          const bool out = ((!keepx) | LaneCorners<D>::leaves(c, dl)) &
+                           ((skip_zero == 0) | (acc[c] != 0.0f));
           flush(out, idx[c], acc[c]);
         }
 #pragma unroll
@@ -817,7 +819,11 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     // loaded row is nonzero in some lane, so no per-sample test remains; the rows whose bit
     // is clear are exactly those the dense walk's per-sample skip passes over, so the same
     // corner sums reach the same entries.
-    __shared__ uint32_t sidx[4][256];
+    constexpr int BS = BSZ;
+    static_assert(BS % 2 == 0, "row indices are read in pairs");
+    // K <= 256 rows, then 2 BS copies of the last set row: a batch (and the prefetch past
+    // the end) reads its BS indices in pairs with no clamp
+    __shared__ __attribute__((aligned(16))) uint32_t sidx[4][256 + 2 * BS];
     uint32_t* my = sidx[threadIdx.x >> 6];
     typedef __attribute__((address_space(4))) const uint32_t cu32;
     int n = 0;
@@ -836,17 +842,32 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_v2_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    constexpr int BS = BSZ;
+    if (n > 0) {
+      const uint32_t last = my[n - 1];
+      if (lane < 2 * BS) my[n + lane] = last;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     typedef __attribute__((address_space(4))) const float cf32;
+    // chunk-relative bases: a row's addresses are 32-bit scalar offsets from them
+    const float* __restrict__ xc = x + m0 * 3;
+    const TG* __restrict__ dc = dout + m0 * 32 + col;
     auto load_rows = [&](int bb, float (*xo)[D], TG* go) {
+      uint32_t r[BS];
+#pragma unroll
+      for (int j = 0; j < BS; j += 2) {
+        const uint2 q = *reinterpret_cast<const uint2*>(my + bb + j);
+        r[j] = q.x;
+        r[j + 1] = q.y;
+      }
 #pragma unroll
       for (int j = 0; j < BS; ++j) {
-        const int k = bb + j < n ? bb + j : n - 1;  // past the end: the last row again (unused)
-        const int64_t m = m0 + __builtin_amdgcn_readfirstlane(static_cast<int>(my[k]));
-        const cf32* xp = (const cf32*)(x + m * 3);
+        const uint32_t i = __builtin_amdgcn_readfirstlane(r[j]);
+        const cf32* xp = (const cf32*)(xc + i * 3u);
 #pragma unroll
         for (int d = 0; d < D; ++d) xo[j][d] = xp[d];
-        go[j] = dout[m * 32 + col];
+        go[j] = dc[i * 32u];
       }
     };
     if (n > 0) {

@@ -91,7 +91,8 @@ def pmc_entry(pmc: dict, tag: str, key_sfx: str):
 
 
 def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
-                  requests: int | None = None) -> dict:
+                  requests: int | None = None, nz_rows: float | None = None,
+                  dir_tiles: float | None = None) -> dict:
     """Algorithmic work per launch of each hot kernel.
 
     ``bytes`` = compulsory HBM traffic (every per-sample stream read or written once, the
@@ -103,7 +104,19 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
     (hash backward) = memory-side f32 atomic requests per launch, counted in the run
     (``requests``, count_hash_requests) or else from rocprofv3 PMC
     (profiles/pmc_traffic.json), priced against the measured request ceiling.
+
+    Reference numerics with row bits (r06, field.py ``_ROW_BITS``): the field backward
+    writes f16 dL/denc rows plus one bit per row, and the hash-grid backward reads the bits
+    and only the rows with a nonzero value (``nz_rows``: their fraction, measured in the
+    run). The field backward skips the dir network on 32-row tiles whose dL/dcolor is zero
+    (``dir_tiles``: the fraction of tiles that still walk it, measured in the run), so its
+    ``flops`` count the work it does (the pos network, plus the dir network on those
+    tiles); ``flops_full`` is tinycudann's full backward beside it.
     """
+    from atmonr_amd import field as _field
+
+    ref_rows = (getattr(pipe, "numerics", None) == "reference" and _field._ROW_BITS
+                and not _field._TILE_SKIP and pipe.pos_encoder.hash_grids[0].n_out == 32)
     grid = pipe.pos_encoder.hash_grids[0]
     n_table = grid.desc.n_params                # f16 table entries x features
     pos, dirm = pipe.pos_mlp.desc, pipe.dir_mlp.desc
@@ -115,10 +128,18 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
     f_fwd = mlp_flops(pos) + mlp_flops(dirm)
     nb = dirm.n_output
     enc_b = 2 * grid.n_out                      # f16 features
+    denc_b = 2 * grid.n_out if ref_rows else 4 * grid.n_out  # dL/denc row: f16 / f32
+    bits_b = 1.0 / 8 if ref_rows else 0.0                     # row bits
+    rows_read = nz_rows if (ref_rows and nz_rows is not None) else 1.0
+    dir_frac = dir_tiles if (getattr(pipe, "numerics", None) == "reference"
+                             and dir_tiles is not None) else 1.0
+    f_bwd = 2 * (mlp_flops(pos) + dir_frac * mlp_flops(dirm))
+    f_rec = mlp_flops(pos) + dir_frac * mlp_flops(dirm)
     out = {
         "hash_fwd": {"bytes": M * (12 + enc_b) + 2 * n_table, "flops": 0.0,
                      "survey_bytes": M * (12 + grid.n_levels * 8 * 2 * 2 + enc_b)},
-        "hash_bwd": {"bytes": M * (12 + 4 * grid.n_out) + 8 * n_table, "flops": 0.0,
+        "hash_bwd": {"bytes": M * (bits_b + rows_read * (12 + denc_b)) + 8 * n_table,
+                     "flops": 0.0,
                      "survey_bytes": M * (64 + 12 + 2 * grid.n_levels * 8 * 2 * 2)},
         # enc in, sigma + color out
         "field_fwd": {"bytes": M * (enc_b + 4 + 4 * nb), "flops": M * f_fwd},
@@ -129,11 +150,16 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
                            "survey_bytes": M * (12 + grid.n_levels * 8 * 2 * 2 + enc_b + 4 + 4 * nb)},
         # enc in, sigma out; the pos MLP only (extract / occupancy)
         "field_density": {"bytes": M * (enc_b + 4), "flops": M * mlp_flops(pos)},
-        # enc + dL/dcolor + dL/dsigma in, f32 dL/denc out; dX + dW (2x the forward) is the
-        # algorithmic work, the forward the kernel recomputes is reported beside it
-        "field_bwd": {"bytes": M * (enc_b + 4 * nb + 4 + 4 * grid.n_out), "flops": 2 * M * f_fwd,
-                      "flops_with_recompute": 3 * M * f_fwd},
+        # enc + dL/dcolor + dL/dsigma in, dL/denc (+ row bits) out; dX + dW (2x the forward)
+        # is the algorithmic work, the forward the kernel recomputes is reported beside it
+        "field_bwd": {"bytes": M * (enc_b + 4 * nb + 4 + denc_b + bits_b), "flops": M * f_bwd,
+                      "flops_with_recompute": M * (f_bwd + f_rec)},
     }
+    if dir_frac < 1.0:
+        out["field_bwd"]["flops_full"] = 2 * M * f_fwd
+        out["field_bwd"]["dir_tiles_frac"] = dir_frac
+    if ref_rows:
+        out["hash_bwd"]["rows_read_frac"] = rows_read
     ent, stale = pmc_entry(pmc, "hash_bwd", key_sfx)
     if requests is not None:
         out["hash_bwd"]["atomic_requests"] = float(requests)
@@ -156,7 +182,7 @@ def kernel_models(pipe, M: int, pmc: dict | None = None, key_sfx: str = "",
     return out
 
 
-def count_hash_requests(job, n_samples: int) -> tuple[int, float, float] | None:
+def count_hash_requests(job, n_samples: int) -> tuple[int, float, float, float] | None:
     """Memory-side atomic requests of the hash-grid backward in one benched step: one
     eager step of the job keeps the hash-grid backward's inputs (coordinates, dL/denc,
     gradient buffer), and the instrumented launch anr_hashgrid_bwd_count_requests replays
@@ -164,7 +190,8 @@ def count_hash_requests(job, n_samples: int) -> tuple[int, float, float] | None:
     zero-sum corners the kernel skips included, so the count follows the numerics (most
     f16 dL/denc underflow in reference numerics). Returns (requests, fraction of nonzero
     dL/denc in that step: is the field alive?, fraction of samples with any nonzero
-    dL/denc); None when the pipeline has no fused v2-eligible hash grid."""
+    dL/denc, fraction of 32-row tiles with a nonzero dL/dcolor); None when the pipeline
+    has no fused v2-eligible hash grid."""
     from atmonr_amd import _lib
 
     pipe = job.pipe
@@ -207,8 +234,15 @@ def count_hash_requests(job, n_samples: int) -> tuple[int, float, float] | None:
     nz = (d_enc != 0).float().mean().item()
     # sample granularity (what the walker skips since r05): rows with any nonzero value
     nz_rows = (d_enc != 0).any(1).float().mean().item()
+    # 32-row tiles with a nonzero dL/dcolor (the reference numerics' field backward walks
+    # the dir network on those only)
+    dc_ = pipe._last_field_grads[1]
+    M_ = dc_.shape[0]
+    dc_nz = (dc_.reshape(M_, -1) != 0).any(1)
+    dc_nz = torch.nn.functional.pad(dc_nz, (0, -M_ % 32)).view(-1, 32).any(1)
+    dir_tiles = dc_nz.float().mean().item()
     del pipe._last_hash_bwd, pipe._last_d_enc, pipe._last_field_grads
-    return int(cnt.item()), nz, nz_rows
+    return int(cnt.item()), nz, nz_rows, dir_tiles
 
 
 def _roof(mdl: dict, avg_ms: float, peaks: dict, mfma_key: str) -> dict:
@@ -956,7 +990,9 @@ def main():
                f"{rank_batch}x{args.samples}")
     req = count_hash_requests(job, args.samples) if occ is None else None
     nreq = None if req is None else req[0]
-    models = kernel_models(pipe, M, pmc, pmc_sfx, requests=nreq)
+    models = kernel_models(pipe, M, pmc, pmc_sfx, requests=nreq,
+                           nz_rows=None if req is None else req[2],
+                           dir_tiles=None if req is None else req[3])
     kernels, dominant = {}, None
     if not args.no_kernel_timer:
         kernels = job.profile(args.profile_steps, models, peaks, mfma_key)
@@ -1021,6 +1057,17 @@ def main():
             hb["atomic_requests_before_after"] = [req[0], req2[0]]
             hb["d_enc_nonzero_before_after"] = [round(req[1], 4), round(req2[1], 4)]
             hb["d_enc_nonzero_rows_before_after"] = [round(req[2], 4), round(req2[2], 4)]
+            # the row-bit walker's bytes and the field backward's dir-network work follow
+            # the same drift: price them at the mean of the two states as well
+            m2 = kernel_models(pipe, M, nz_rows=0.5 * (req[2] + req2[2]),
+                               dir_tiles=0.5 * (req[3] + req2[3]))
+            for k in ("hash_bwd", "field_bwd"):
+                for f in ("bytes", "flops", "flops_with_recompute", "rows_read_frac",
+                          "dir_tiles_frac"):
+                    if f in m2[k]:
+                        models[k][f] = m2[k][f]
+            models["field_bwd"]["d_color_nonzero_tiles_before_after"] = [
+                round(req[3], 4), round(req2[3], 4)]
 
     strong = None
     if world > 1 and scaling == "weak" and not args.no_strong and args.batch % world == 0:
@@ -1125,6 +1172,10 @@ def main():
                             "mfma_frac_with_recompute") if x in k}}
             if mdl.get("flops_with_recompute"):
                 roofline["algorithmic_flops_with_recompute"] = mdl["flops_with_recompute"]
+            for x in ("flops_full", "dir_tiles_frac", "d_color_nonzero_tiles_before_after",
+                      "rows_read_frac"):
+                if x in mdl:
+                    roofline[x] = mdl[x]
             if st.get("source"):
                 roofline["timing_source"] = st["source"]
             if "atomic_requests" in mdl:
@@ -1185,6 +1236,7 @@ def main():
             "transient_window": transient,
             "d_enc_nonzero_frac": None if req is None else round(req[1], 4),
             "d_enc_nonzero_rows_frac": None if req is None else round(req[2], 4),
+            "d_color_nonzero_tiles_frac": None if req is None else round(req[3], 4),
             "graph": job.graphed,
             "data": f"synthetic ({args.views}-view {args.img_size}x{args.img_size} "
                     f"HARP2-shaped scene, {len(ds)} rays; random-init weights)",

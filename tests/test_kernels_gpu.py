@@ -1392,6 +1392,67 @@ def test_ingp_field_bwd_ref16_rows_equals_f32_rows(dev, nb, n_per_ray, R):
         assert (a_ - b_).abs().max().item() <= 2e-5 * b_.abs().max().item()
 
 
+@pytest.mark.parametrize("rows", [False, True])
+@pytest.mark.parametrize("n_per_ray,R", [(64, 40), (1024, 12)])
+def test_ingp_field_bwd_ref16_zero_color_tiles_skip_dir_net(dev, rows, n_per_ray, R):
+    """Reference numerics (r06): a 32-row tile whose dL/dcolor is zero in every row skips
+    the dir network's backward and the dir half of the forward recompute. Against the same
+    launch with those zeros replaced by 1e-30 (nonzero, so the tile walks the dir network,
+    whose f16 chain rounds them to exactly 0): dL/denc and the row bits are bit-identical and
+    the parameter gradients agree up to the atomic flush order. Rays with ordinary colour
+    gradients and rays with none (dL/dsigma too) are mixed in."""
+    from atmonr_amd import _lib
+
+    width, nhd, nb = 64, 2, 4
+    M = R * n_per_ray
+    g = torch.Generator(device=dev).manual_seed(12)
+    lib = _lib.load()
+    pdsc, ddsc = _lib.mlp_desc(32, 16, width, 1, False), _lib.mlp_desc(19, nb, width, nhd, False)
+    pb, db = ctypes.byref(pdsc), ctypes.byref(ddsc)
+    pp = torch.randn(lib.anr_mlp_n_params(pb), device=dev, generator=g) * (2.0 / 32) ** 0.5
+    pd = torch.randn(lib.anr_mlp_n_params(db), device=dev, generator=g) * (2.0 / width) ** 0.5
+    enc = (torch.rand(M, 32, device=dev, generator=g) * 2 - 1).half()
+    dirs = torch.rand(R, 3, device=dev, generator=g)
+    s = _lib.stream(dev)
+    packed = torch.empty(lib.anr_ingp_field_packed_size(pb, db), device=dev, dtype=torch.float16)
+    _lib.call("anr_ingp_field_pack", pb, db, _lib.F16, pp.data_ptr(), pd.data_ptr(),
+              packed.data_ptr(), s)
+    dsig = (torch.randn(M, device=dev, generator=g) * 1e-3).half().float()
+    dcol = torch.zeros(M, nb, device=dev)
+    for r in range(0, R, 4):  # ordinary colour gradients on every 4th ray
+        dcol[r * n_per_ray:(r + 1) * n_per_ray] = torch.randn(n_per_ray, nb, device=dev,
+                                                              generator=g) * 1e-2
+    dsig[n_per_ray:2 * n_per_ray] = 0.0  # ray 1: no gradient at all
+    tiny = torch.where(dcol == 0, torch.full_like(dcol, 1e-30), dcol)
+    outs = []
+    for dc in (dcol, tiny):
+        g_pos, g_dir = torch.zeros_like(pp), torch.zeros_like(pd)
+        bits = None
+        if rows:
+            d_enc = torch.full((M, 32), float("nan"), device=dev, dtype=torch.float16)
+            bits = torch.zeros(-(-M // 32), device=dev, dtype=torch.int32)
+            _lib.call("anr_ingp_field_bwd_ref16_rows", pb, db, packed.data_ptr(), enc.data_ptr(),
+                      32, dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dc.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), 128.0,
+                      bits.data_ptr(), s)
+        else:
+            d_enc = torch.full((M, 32), float("nan"), device=dev)
+            _lib.call("anr_ingp_field_bwd_ref16", pb, db, packed.data_ptr(), enc.data_ptr(), 32,
+                      dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dc.data_ptr(), nb,
+                      d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), 128.0, s)
+        outs.append((d_enc, bits, g_pos, g_dir))
+    torch.cuda.synchronize()
+    (da, ba, gpa, gda), (db_, bb, gpb, gdb) = outs
+    assert not torch.isnan(da).any()
+    assert torch.equal(da, db_)
+    assert (da != 0).any()
+    if rows:
+        assert torch.equal(ba, bb)
+    assert (gpa - gpb).abs().max().item() <= 1e-5 * gpb.abs().max().item()
+    assert (gda - gdb).abs().max().item() <= 1e-5 * gdb.abs().max().item()
+    assert gdb.abs().max().item() > 0  # the rays with colour gradients reached the dir net
+
+
 @pytest.mark.parametrize("M", [262144, 1048576, 300000, 8192 * 1024])
 def test_hashgrid_bwd_rows_equals_plain(dev, M):
     """anr_hashgrid_bwd_rows (r06, ABI 5) walks only the rows whose bit is set: with f16

@@ -5,7 +5,8 @@ accumulators in AGPRs, `mma32_acc*`) and a ReLU mask from asm; hipcc's hazard re
 pads nothing inside an asm statement, so the kernels carry hand-placed `s_nop`s. r02
 shipped one missing pair (a VALU-written MFMA operand read at once: launch-to-launch
 different dW). This tool reads the built device code back and checks,
-per kernel, in program order (straight-line; a label restarts the window):
+per kernel, in program order (straight-line; a label, a branch target or an
+unconditional branch restarts the window):
 
 * VALU write of a VGPR -> MFMA reading it as SrcA / SrcB / SrcC: >= 2 wait states between;
 * MFMA write of a VGPR / AGPR -> VALU (incl. v_accvgpr_read / _mov) reading it as a
@@ -87,24 +88,52 @@ def waits(mn: str, ops) -> int:
     return 1
 
 
+_ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
+_TARGET = re.compile(r"<(.+)\+0x([0-9a-f]+)>")
+_ENDS = ("s_branch", "s_setpc_b64", "s_endpgm")
+
+
 def blocks(asm: str):
-    """(kernel, [(mnemonic, operands, text)]) straight-line blocks in program order."""
+    """(kernel, [(mnemonic, operands, text)]) straight-line blocks in program order. A
+    block ends at a label, at an unconditional branch / return, and before any address a
+    branch jumps to (llvm-objdump prints no labels for those: the targets are read from
+    the branches' `<kernel+0x...>` annotations); code after an `s_branch` is reached only
+    by a jump, so an MFMA's result window never runs across it."""
+    starts, targets = {}, set()
+    for raw in asm.splitlines():
+        s = raw.strip()
+        m = re.match(r"^([0-9a-f]+) <(.+)>:$", s)
+        if m:
+            starts[m.group(2)] = int(m.group(1), 16)
+    for raw in asm.splitlines():
+        t = _TARGET.search(raw)
+        if t and t.group(1) in starts and raw.strip().startswith("s_"):
+            targets.add(starts[t.group(1)] + int(t.group(2), 16))
     out, kernel, block = [], "?", []
+
+    def flush():
+        nonlocal block
+        if block:
+            out.append((kernel, block))
+        block = []
+
     for raw in asm.splitlines():
         s = raw.strip()
         m = re.match(r"^[0-9a-f]+ <(.+)>:$", s)
         if m or s.endswith(":") or s.startswith("<"):
-            if block:
-                out.append((kernel, block))
-            block = []
+            flush()
             if m:
                 kernel = m.group(1)
-            continue  # a branch target restarts the window
+            continue  # a label restarts the window
+        a = _ADDR.search(s)
+        if a and int(a.group(1), 16) in targets:
+            flush()  # a branch target restarts the window
         p = parse(s)
         if p:
             block.append((p[0], p[1], s.split("//")[0].strip()))
-    if block:
-        out.append((kernel, block))
+            if p[0] in _ENDS:
+                flush()
+    flush()
     return out
 
 

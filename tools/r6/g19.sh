@@ -1,0 +1,7 @@
+#!/bin/bash
+# r6: the whole GPU suite after the row-bit hash-grid backward (ABI 5)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r6_g19; mkdir -p $O
+ANR_PSNR_OUT=$O/psnr_nerf.json ANR_INGP_PSNR_OUT=$O/psnr.json timeout -k 10 1140 python -u -m pytest tests -m gpu -x -q --timeout 1000 --timeout-method thread --durations=25 > $O/test_gpu.log 2>&1 || { tail -40 $O/test_gpu.log; exit 1; }
+tail -n 32 $O/test_gpu.log

@@ -316,8 +316,9 @@ _SIGNATURES = {
     "anr_ingp_field_bwd_ref16_rows": (
         c_int32,
         [POINTER(MlpDesc), POINTER(MlpDesc), _P, _P, c_int64, _P, c_int64, c_int64, _P, _P,
-         c_int64, _P, c_int64, _P, _P, c_float, _P, _P],
+         c_int64, _P, c_int64, _P, _P, c_float, _P, _P, c_int64, _P],
     ),
+    "anr_ingp_field_bwd_ref16_rows_workspace_bytes": (c_int64, [c_int64]),
     "anr_mlp_bwd_ref16": (
         c_int32,
         [POINTER(MlpDesc), _P, _P, c_int32, c_int64, c_int64, _P, c_int32, c_int64, _P,

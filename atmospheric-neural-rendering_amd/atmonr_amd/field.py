@@ -212,10 +212,16 @@ class IngpFieldFn(torch.autograd.Function):
             # loaded, the per-sample zero test (the r05 form, A/B)
             d_enc = torch.empty(M, n_enc, device=dev, dtype=torch.float16)
             row_nz = torch.empty((M + 31) // 32, device=dev, dtype=torch.int32)
+            # with a workspace: a pos pass over the tiles whose dL/dcolor is zero (every tile
+            # once training settles: the dir network adds exactly 0 there) at two waves per
+            # SIMD, and a full pass over the tiles it lists. ANR_POS_PASS=0: one kernel
+            ws_bytes = _lib.load().anr_ingp_field_bwd_ref16_rows_workspace_bytes(M) if _POS_PASS else 0
+            ws = torch.empty(max(1, ws_bytes), device=dev, dtype=torch.uint8) if ws_bytes else None
             call("anr_ingp_field_bwd_ref16_rows", pdesc, ddesc, ptr(packed), ptr(enc),
                  ctx.enc_ld, ptr(dirs), ctx.n_per_ray, M, ptr(d_sigma), ptr(d_color),
                  d_color.stride(0), ptr(d_enc), d_enc.stride(0), ptr(g_pos), ptr(g_dir),
-                 float(ls), ptr(row_nz), s, tag="field_bwd")
+                 float(ls), ptr(row_nz), None if ws is None else ptr(ws), ws_bytes, s,
+                 tag="field_bwd")
         elif ls:
             d_enc = torch.empty(M, n_enc, device=dev, dtype=torch.float32)
             # reference numerics: tcnn's loss-scaled f16 backward. ANR_TILE_SKIP=1: it also
@@ -299,6 +305,7 @@ _ENC_PLANES = os.environ.get("ANR_ENC_PLANES", "1") != "0"
 _HASH_FIELD = os.environ.get("ANR_HASH_FIELD", "0") != "0"
 _TILE_SKIP = os.environ.get("ANR_TILE_SKIP", "0") != "0"
 _ROW_BITS = os.environ.get("ANR_ROW_BITS", "1") != "0"
+_POS_PASS = os.environ.get("ANR_POS_PASS", "1") != "0"
 
 
 def field_fused(pipe) -> bool:

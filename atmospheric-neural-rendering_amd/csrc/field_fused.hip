@@ -284,6 +284,9 @@ struct Args {
   // tile a word of row bits, bit i set when row 32 t + i has a nonzero value
   _Float16* d_enc_h;
   uint32_t* row_nz;
+  // its pos / list passes (workspace): the tiles with a nonzero dL/dcolor and their count
+  int32_t* tile_list;
+  uint32_t* tile_count;
 };
 
 // ROWS is a compile-time choice: a run-time test on a.rows in the prefetch paths put a
@@ -1045,11 +1048,19 @@ __device__ __forceinline__ h4 tr_b(h8 x, h8 sel) {
 // REF 2 (anr_ingp_field_bwd_ref16_rows): the same arithmetic, dL/denc written as f16 (its
 // values are f16 numbers already, so the rows hold them exactly) plus one bit per row, set
 // when any of the row's 32 values is nonzero (a.row_nz, one 32-bit word per 32-row tile)
+// REF 4 (the pos pass of anr_ingp_field_bwd_ref16_rows with a workspace): REF 2 on the
+// tiles whose dL/dcolor is zero in every row -- the pos network only, so the dir network's
+// registers, dW accumulators and LDS sums are not part of the kernel and more waves fit a
+// SIMD -- while a tile with a nonzero dL/dcolor is appended to a.tile_list (a.tile_count)
+// and left alone. REF 3 (the list pass, launched after it): REF 2 on exactly the listed
+// tiles (count read on the device), the whole network.
 template <int W, int NHD, bool FAST, bool ROWS, bool BF, int REF = 0>
 __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64_t tpw,
                                                      const float* wmax) {
   static_assert(!(REF && BF), "reference numerics are f16");
-  constexpr bool RMASK = REF == 2;
+  static_assert(REF < 3 || FAST, "the pos / list passes use the fast d_color layout");
+  constexpr bool RMASK = REF >= 2;
+  constexpr bool POS = REF == 4;  // no dir network in this kernel
   // MT 16-sample halves per tile, the dW contraction over NP pairs of them. (64-sample
   // tiles, MT = 4, measured 6 % slower at the same 1 wave/SIMD: profiles/r03_field_bwd_ab.log)
   constexpr int MT = 2, TR = 16 * MT, NP = MT / 2;
@@ -1058,12 +1069,13 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
   // the block's dW partials (pos parameters, then dir), summed here before the one global
   // flush per block
-  __shared__ float red[N::NPOS + N::NDIR];
+  __shared__ float red[POS ? N::NPOS : N::NPOS + N::NDIR];
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int waves = blockDim.x >> 6, wave = threadIdx.x >> 6;
   for (int e = threadIdx.x * 8; e < N::n_packed; e += blockDim.x * 8)
     *reinterpret_cast<h8*>(wsm + e) = *reinterpret_cast<const h8*>(a.packed + e);
-  for (int e = threadIdx.x; e < N::NPOS + N::NDIR; e += blockDim.x) red[e] = 0.0f;
+  constexpr int NRED = POS ? N::NPOS : N::NPOS + N::NDIR;
+  for (int e = threadIdx.x; e < NRED; e += blockDim.x) red[e] = 0.0f;
   __syncthreads();
   // per-tile opaque copy of the fragment base: the weight fragments are re-read from LDS
   // each tile instead of being hoisted into registers
@@ -1310,6 +1322,12 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
               cur[mt].dc[3] != 0.0f;
       dir_walk = __any(cnz);
     }
+    if constexpr (POS) {
+      if (dir_walk) {  // the list pass takes this tile (d_enc rows and bits included)
+        if (lane == 0) a.tile_list[atomicAdd(a.tile_count, 1u)] = static_cast<int32_t>(tile);
+        return;
+      }
+    }
     // ---- forward recompute of both 16-sample halves; every activation stays in registers
     Tile<W, NHD> t[MT];
     h4 gc[MT];
@@ -1319,8 +1337,8 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) valid[mt] = full || tile * TR + mt * 16 + li < a.M;
       FwdWeights<W, NHD> fwl;
-      fwl.load(wbt, lane, dir_walk);
-      tile_forward<W, NHD, MT, BF>(fwl, cur, valid, g, t, NoSink{}, dir_walk);
+      fwl.load(wbt, lane, !POS && dir_walk);
+      tile_forward<W, NHD, MT, BF>(fwl, cur, valid, g, t, NoSink{}, !POS && dir_walk);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         dens[mt] = (REF ? r16(t[mt].po[0]) : t[mt].po[0]) > 0.0f;
@@ -1332,7 +1350,7 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
       }
     }
     h4 dpo[MT];
-    if (dir_walk) {
+    if (!POS && dir_walk) {
       auto last = [&](int mt, int kt) -> h4 { return NHD == 2 ? t[mt].hd1[kt] : t[mt].hd0[kt]; };
       // ---- dir output layer: dW_D2 (16 x W) += gc^T · X_last ; dX_last = D2^T gc
       // Each layer's W^T fragments are read from LDS at the start of the layer and pinned
@@ -1531,31 +1549,46 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
     // the last dW MFMAs of the tile have written their accumulators before anything
     // (a loop-exit copy) reads them
     agpr_fence();
-    agpr_pin(dD2);
-    agpr_pin(dD1);
-    agpr_pin(dD0);
+    if constexpr (!POS) {
+      agpr_pin(dD2);
+      agpr_pin(dD1);
+      agpr_pin(dD0);
+    }
     agpr_pin(dP1);
     agpr_pin(dP0);
   };
-  {
-    const std::integral_constant<bool, true> full_tile;
-    int64_t tile = t_begin;
-    for (; tile + 1 < t_full_end; tile += 2) {
-      process(full_tile, tile, nr0, nr1);
-      process(full_tile, tile + 1, nr1, nr0);
+  if constexpr (REF == 3) {
+    // the listed tiles, strided over the grid's wavefronts (the general per-tile path: a
+    // listed tile's neighbours are not this wave's)
+    const int64_t nw = static_cast<int64_t>(gridDim.x) * waves;
+    const int64_t cnt = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<int>(*a.tile_count)));
+    for (int64_t i = w_id; i < cnt; i += nw)
+      process(std::integral_constant<bool, false>{},
+              static_cast<int64_t>(__builtin_amdgcn_readfirstlane(a.tile_list[i])), nr0, nr1);
+  } else {
+    {
+      const std::integral_constant<bool, true> full_tile;
+      int64_t tile = t_begin;
+      for (; tile + 1 < t_full_end; tile += 2) {
+        process(full_tile, tile, nr0, nr1);
+        process(full_tile, tile + 1, nr1, nr0);
+      }
+      if (tile < t_full_end) process(full_tile, tile, nr0, nr1);
+      if constexpr (FAST) {
+        if (t_begin < t_full_end) store_pend();
+      }
     }
-    if (tile < t_full_end) process(full_tile, tile, nr0, nr1);
-    if constexpr (FAST) {
-      if (t_begin < t_full_end) store_pend();
-    }
+    for (int64_t tile = t_full_end > t_begin ? t_full_end : t_begin; tile < t_end; ++tile)
+      process(std::integral_constant<bool, false>{}, tile, nr0, nr1);
   }
-  for (int64_t tile = t_full_end > t_begin ? t_full_end : t_begin; tile < t_end; ++tile)
-    process(std::integral_constant<bool, false>{}, tile, nr0, nr1);
 
   agpr_fence();
-  agpr_pin(dD2);
-  agpr_pin(dD1);
-  agpr_pin(dD0);
+  if constexpr (!POS) {
+    agpr_pin(dD2);
+    agpr_pin(dD1);
+    agpr_pin(dD0);
+  }
   agpr_pin(dP1);
   agpr_pin(dP0);
   // dW flush: each wavefront's partials (unscaled by its own gradient scale) go into the
@@ -1571,10 +1604,10 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   };
 #pragma unroll
   for (int kt = 0; kt < NT; ++kt) {
-    flush(rdir + N::D2, W, dD2[kt], 0, 16 * kt + li);
+    if constexpr (!POS) flush(rdir + N::D2, W, dD2[kt], 0, 16 * kt + li);
     flush(rpos + N::P1, W, dP1[kt], 0, 16 * kt + li);
   }
-  if constexpr (NHD == 2) {
+  if constexpr (NHD == 2 && !POS) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -1584,11 +1617,11 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
-      flush(rdir + N::D0, 32, dD0[nt * 2 + kt], 16 * nt, dir_col(16 * kt + li));
+      if constexpr (!POS) flush(rdir + N::D0, 32, dD0[nt * 2 + kt], 16 * nt, dir_col(16 * kt + li));
       flush(rpos + N::P0, 32, dP0[nt * 2 + kt], 16 * nt, 16 * kt + li);
     }
   __syncthreads();
-  for (int e = threadIdx.x; e < N::NPOS + N::NDIR; e += blockDim.x) {
+  for (int e = threadIdx.x; e < NRED; e += blockDim.x) {
     const float v = red[e];
     if (v != 0.0f) atomicAdd(e < N::NPOS ? a.g_pos + e : a.g_dir + (e - N::NPOS), v);
   }
@@ -1629,6 +1662,37 @@ static BwdGeom bwd_geom(int64_t M, bool fast) {
   if (blocks < 1) blocks = 1;
   const int64_t nw = blocks * waves;
   return {blocks, nw, (tiles + nw - 1) / nw};
+}
+
+// the reference-numerics pos pass (REF 4): its own occupancy (no dir network's registers
+// or LDS sums); the list pass (REF 3): one block per CU slot of its occupancy
+template <int W, int NHD>
+static BwdGeom pos_geom(int64_t M) {
+  const int waves = 4;
+  static int p = 0;
+  if (p == 0) {
+    int nb = 0;
+    const void* fn = reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, true, false, false, 4>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * waves, 0) != hipSuccess || nb < 1) nb = 1;
+    p = nb;
+  }
+  const int64_t tiles = (M + 31) / 32;
+  int64_t blocks = (tiles + waves - 1) / waves;
+  if (blocks > 256LL * p) blocks = 256LL * p;
+  if (blocks < 1) blocks = 1;
+  const int64_t nw = blocks * waves;
+  return {blocks, nw, (tiles + nw - 1) / nw};
+}
+template <int W, int NHD>
+static int64_t list_blocks() {
+  static int p = 0;
+  if (p == 0) {
+    int nb = 0;
+    const void* fn = reinterpret_cast<const void*>(&bwd_rt_kernel<W, NHD, true, false, false, 3>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, 0) != hipSuccess || nb < 1) nb = 1;
+    p = nb;
+  }
+  return 256LL * p;
 }
 
 template <int W, int NHD, bool BF>
@@ -1694,7 +1758,19 @@ static int run(int op, const Args& a, float* ws, int64_t ws_bytes, hipStream_t s
 #define ANR_REF_BWD(FASTV, REFV)                                                             \
   hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, FASTV, false, false, REFV>), grid, block, 0, st, a, \
                      0.0f, gm.tpw, nullptr)
-      if (a.d_enc_h) {
+      if (a.d_enc_h && fast && a.tile_list) {
+        // the pos pass over every tile (more waves per SIMD: no dir network in it), then the
+        // list pass over the tiles it left (nonzero dL/dcolor), at most one per wavefront
+        // of a grid of its occupancy
+        const BwdGeom pg = pos_geom<W, NHD>(a.M);
+        if (hipMemsetAsync(a.tile_count, 0, sizeof(uint32_t), st) != hipSuccess) return 1;
+        hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, true, false, false, 4>),
+                           dim3(static_cast<unsigned>(pg.blocks)), block, 0, st, a, 0.0f, pg.tpw,
+                           nullptr);
+        hipLaunchKernelGGL((bwd_rt_kernel<W, NHD, true, false, false, 3>),
+                           dim3(static_cast<unsigned>(list_blocks<W, NHD>())), block, 0, st, a,
+                           0.0f, int64_t{0}, nullptr);
+      } else if (a.d_enc_h) {
         if (fast) ANR_REF_BWD(true, 2);
         else ANR_REF_BWD(false, 2);
       } else {
@@ -2013,7 +2089,7 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
                      int64_t d_enc_stride, float* g_pos, float* g_dir, void* workspace,
                      int64_t workspace_bytes, anr_stream_t stream, float loss_scale = 0.0f,
                      uint8_t* tile_nz = nullptr, void* d_enc_h = nullptr,
-                     uint32_t* row_nz = nullptr) {
+                     uint32_t* row_nz = nullptr, void* tiles_ws = nullptr) {
   const int v = variant(pos, dir);
   ANR_CHECK_ARG(v != 0, "anr_ingp_field_bwd: unsupported pos/dir MLP pair");
   ANR_CHECK_ARG(loss_scale == 0.0f || (loss_scale > 0.0f && mma_dtype == ANR_F16 && rows == nullptr),
@@ -2054,6 +2130,10 @@ static int field_bwd(const anr_mlp_desc* pos, const anr_mlp_desc* dir, int32_t m
   a.tile_nz = tile_nz;
   a.d_enc_h = static_cast<_Float16*>(d_enc_h);
   a.row_nz = row_nz;
+  if (tiles_ws) {  // ref16_rows_workspace_bytes: the count, then one int32 per 32-row tile
+    a.tile_count = static_cast<uint32_t*>(tiles_ws);
+    a.tile_list = reinterpret_cast<int32_t*>(static_cast<char*>(tiles_ws) + 256);
+  }
   const int rc = dispatch(v, mma_dtype == ANR_BF16, 2, a, static_cast<float*>(workspace),
                           workspace_bytes, reinterpret_cast<hipStream_t>(stream));
   ANR_CHECK_ARG(rc != 2,
@@ -2139,6 +2219,10 @@ extern "C" int anr_ingp_field_bwd_ref16_tiles(const anr_mlp_desc* pos, const anr
                    0, stream, loss_scale, tile_nz);
 }
 
+extern "C" int64_t anr_ingp_field_bwd_ref16_rows_workspace_bytes(int64_t M) {
+  return M <= 0 ? 0 : 256 + 4 * ((M + 31) / 32);
+}
+
 extern "C" int anr_ingp_field_bwd_ref16_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
                                              const void* packed, const void* enc,
                                              int64_t enc_stride, const float* dirs,
@@ -2146,13 +2230,20 @@ extern "C" int anr_ingp_field_bwd_ref16_rows(const anr_mlp_desc* pos, const anr_
                                              const float* d_color, int64_t d_color_stride,
                                              void* d_enc_h, int64_t d_enc_stride, float* g_pos,
                                              float* g_dir, float loss_scale, uint32_t* row_nz,
+                                             void* workspace, int64_t workspace_bytes,
                                              anr_stream_t stream) {
   ANR_CHECK_ARG(loss_scale > 0.0f, "anr_ingp_field_bwd_ref16_rows: loss_scale must be > 0");
   ANR_CHECK_ARG(d_enc_h != nullptr && row_nz != nullptr,
                 "anr_ingp_field_bwd_ref16_rows: null d_enc / row_nz");
+  ANR_CHECK_ARG(workspace == nullptr ||
+                    workspace_bytes >= anr_ingp_field_bwd_ref16_rows_workspace_bytes(M),
+                "anr_ingp_field_bwd_ref16_rows: workspace smaller than "
+                "anr_ingp_field_bwd_ref16_rows_workspace_bytes()");
+  ANR_CHECK_ARG((reinterpret_cast<uintptr_t>(workspace) & 255) == 0,
+                "anr_ingp_field_bwd_ref16_rows: workspace must be 256-byte aligned");
   return field_bwd(pos, dir, ANR_F16, packed, enc, enc_stride, dirs, n_per_ray, M, nullptr,
                    d_sigma, d_color, d_color_stride, nullptr, d_enc_stride, g_pos, g_dir, nullptr,
-                   0, stream, loss_scale, nullptr, d_enc_h, row_nz);
+                   0, stream, loss_scale, nullptr, d_enc_h, row_nz, workspace);
 }
 
 extern "C" int anr_ingp_field_fwd_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,

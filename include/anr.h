@@ -607,14 +607,20 @@ int anr_ingp_field_bwd_ref16_tiles(const anr_mlp_desc* pos, const anr_mlp_desc* 
  * stride d_enc_stride, 8-byte aligned; the reference numerics' dL/denc values are f16
  * numbers, tinycudann/modules.py casts them to the f16 input's dtype, so the rows hold them
  * exactly) and one bit per row in row_nz (ceil(M / 32) words): bit (m % 32) of word m / 32
- * set iff row m has a nonzero value. For anr_hashgrid_bwd_rows (ABI 5). */
+ * set iff row m has a nonzero value. For anr_hashgrid_bwd_rows (ABI 5).
+ * workspace (nullable, 256-byte aligned, anr_ingp_field_bwd_ref16_rows_workspace_bytes(M)
+ * bytes): with it the backward runs as a pos pass over the tiles whose dL/dcolor is zero in
+ * every row (the dir network adds exactly 0 there) and a full pass over the others, listed
+ * in the workspace by the first; the same results. Without it, one kernel does both. */
+int64_t anr_ingp_field_bwd_ref16_rows_workspace_bytes(int64_t M);
 int anr_ingp_field_bwd_ref16_rows(const anr_mlp_desc* pos, const anr_mlp_desc* dir,
                                   const void* packed, const void* enc, int64_t enc_stride,
                                   const float* dirs, int64_t n_per_ray, int64_t M,
                                   const float* d_sigma, const float* d_color,
                                   int64_t d_color_stride, void* d_enc_h, int64_t d_enc_stride,
                                   float* g_pos, float* g_dir, float loss_scale,
-                                  uint32_t* row_nz, anr_stream_t stream);
+                                  uint32_t* row_nz, void* workspace, int64_t workspace_bytes,
+                                  anr_stream_t stream);
 /* anr_mlp_bwd_ws in f16 with tcnn's fixed loss scale: dL/dinput written as
  * f16(f16(g_scaled)/loss_scale). Specialised (fused) MLP shapes only. */
 int anr_mlp_bwd_ref16(const anr_mlp_desc* d, const void* params, const void* in,

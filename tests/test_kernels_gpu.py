@@ -1332,15 +1332,18 @@ def _row_bits(d_enc):
     return torch.where(w >= 2**31, w - 2**32, w).to(torch.int32)
 
 
+@pytest.mark.parametrize("ws", [False, True])
 @pytest.mark.parametrize("nb,n_per_ray,R", [(4, 64, 40), (4, 40, 13), (3, 64, 9), (4, 1024, 24)])
-def test_ingp_field_bwd_ref16_rows_equals_f32_rows(dev, nb, n_per_ray, R):
+def test_ingp_field_bwd_ref16_rows_equals_f32_rows(dev, nb, n_per_ray, R, ws):
     """anr_ingp_field_bwd_ref16_rows (r06, ABI 5) against anr_ingp_field_bwd_ref16 on the
     same inputs: its f16 dL/denc rows hold exactly the f32 path's values (they are f16
     numbers: f16(f16(g_scaled) / 128)), bit for bit; its row bits are exactly the rows with
     a nonzero value; the parameter gradients agree up to the f32 atomic flush order. The
     inputs mix rays whose incoming gradients are zero (skipped tiles), rows whose tiny
     gradients underflow to zero dL/denc in f16, and ordinary rows; a ragged last tile
-    (M = 520) and the general (non-fast) d_color layout (3 outputs) are covered."""
+    (M = 520) and the general (non-fast) d_color layout (3 outputs) are covered. ws: with
+    a workspace (the pos pass + list pass; every tile here has colour gradients, so the
+    pos pass lists them all) and without (one kernel)."""
     from atmonr_amd import _lib
 
     width, nhd = 64, 2
@@ -1371,10 +1374,12 @@ def test_ingp_field_bwd_ref16_rows_equals_f32_rows(dev, nb, n_per_ray, R):
         if rows:
             d_enc = torch.full((M, 32), float("nan"), device=dev, dtype=torch.float16)
             bits = torch.full((-(-M // 32),), -7, device=dev, dtype=torch.int32)
+            wsb = lib.anr_ingp_field_bwd_ref16_rows_workspace_bytes(M) if ws else 0
+            wst = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
             _lib.call("anr_ingp_field_bwd_ref16_rows", pb, db, packed.data_ptr(), enc.data_ptr(),
                       32, dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dcol.data_ptr(), nb,
                       d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), 128.0,
-                      bits.data_ptr(), s)
+                      bits.data_ptr(), wst.data_ptr() if ws else None, wsb, s)
         else:
             d_enc = torch.full((M, 32), float("nan"), device=dev)
             bits = None
@@ -1392,15 +1397,18 @@ def test_ingp_field_bwd_ref16_rows_equals_f32_rows(dev, nb, n_per_ray, R):
         assert (a_ - b_).abs().max().item() <= 2e-5 * b_.abs().max().item()
 
 
-@pytest.mark.parametrize("rows", [False, True])
-@pytest.mark.parametrize("n_per_ray,R", [(64, 40), (1024, 12)])
+@pytest.mark.parametrize("rows", [False, True, "ws"])
+@pytest.mark.parametrize("n_per_ray,R", [(64, 40), (1024, 12), (1024, 300)])
 def test_ingp_field_bwd_ref16_zero_color_tiles_skip_dir_net(dev, rows, n_per_ray, R):
     """Reference numerics (r06): a 32-row tile whose dL/dcolor is zero in every row skips
     the dir network's backward and the dir half of the forward recompute. Against the same
     launch with those zeros replaced by 1e-30 (nonzero, so the tile walks the dir network,
     whose f16 chain rounds them to exactly 0): dL/denc and the row bits are bit-identical and
     the parameter gradients agree up to the atomic flush order. Rays with ordinary colour
-    gradients and rays with none (dL/dsigma too) are mixed in."""
+    gradients and rays with none (dL/dsigma too) are mixed in. rows = "ws": the f16-row
+    kernel with a workspace, i.e. the pos pass (zero-colour tiles) + the list pass (the
+    others), against the same launch on the 1e-30 inputs, where the pos pass lists every
+    tile."""
     from atmonr_amd import _lib
 
     width, nhd, nb = 64, 2, 4
@@ -1431,10 +1439,12 @@ def test_ingp_field_bwd_ref16_zero_color_tiles_skip_dir_net(dev, rows, n_per_ray
         if rows:
             d_enc = torch.full((M, 32), float("nan"), device=dev, dtype=torch.float16)
             bits = torch.zeros(-(-M // 32), device=dev, dtype=torch.int32)
+            wsb = lib.anr_ingp_field_bwd_ref16_rows_workspace_bytes(M) if rows == "ws" else 0
+            wst = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
             _lib.call("anr_ingp_field_bwd_ref16_rows", pb, db, packed.data_ptr(), enc.data_ptr(),
                       32, dirs.data_ptr(), n_per_ray, M, dsig.data_ptr(), dc.data_ptr(), nb,
                       d_enc.data_ptr(), 32, g_pos.data_ptr(), g_dir.data_ptr(), 128.0,
-                      bits.data_ptr(), s)
+                      bits.data_ptr(), wst.data_ptr() if wsb else None, wsb, s)
         else:
             d_enc = torch.full((M, 32), float("nan"), device=dev)
             _lib.call("anr_ingp_field_bwd_ref16", pb, db, packed.data_ptr(), enc.data_ptr(), 32,

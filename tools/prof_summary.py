@@ -45,10 +45,16 @@ TAGS = {  # prefixes: one instantiation of each per bench run (width / dtype fol
     "hash_fwd_v6": "hashgrid_fwd_v6_kernel<3,",
     "hash_field_fwd": "hf_fwd_kernel<64, 2",
     "hash_fwd_v1": "hashgrid_fwd_kernel<3,",
-    "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32, false, 6>",
+    # reference numerics (the headline): the row-bit walker over f16 rows (r06); the build
+    # numerics' dense f32 walker beside it (bench.py's alt_numerics leg)
+    "hash_bwd": "hashgrid_bwd_v2_kernel<3, __half, 3, 32, false, 6, true>",
+    "hash_bwd_build": "hashgrid_bwd_v2_kernel<3, float, 3, 32, false, 6, false>",
     "hash_bwd_rtstride": "hashgrid_bwd_v2_kernel<3, float, 0, 0>",
     "field_fwd": "field::fwd_kernel<",
-    "field_bwd": "field::bwd_rt_kernel<",
+    # reference numerics: the pos pass (zero-colour tiles) and the list pass (r06)
+    "field_bwd": "field::bwd_rt_kernel<64, 2, true, false, false, 4>",
+    "field_bwd_list": "field::bwd_rt_kernel<64, 2, true, false, false, 3>",
+    "field_bwd_build": "field::bwd_rt_kernel<64, 2, true, false, false, 0>",
     "field_bwd_lds": "field::bwd_kernel<",
     "composite_fwd": "rb::fwd_kernel<float, 4, 1, 4>",
     "composite_bwd": "rb::bwd_kernel<float, 4, 1, 4>",

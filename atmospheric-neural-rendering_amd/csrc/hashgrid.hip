@@ -77,7 +77,9 @@ struct LaneCorners {
     }
     // a dense corner sum can reach T only with a corner on the far face or outside the
     // grid: below that every sum is <= res^D - 1 < T (one test per cell, not per corner;
-    // the unsigned max also catches negative cell coordinates)
+    // the unsigned max also catches negative cell coordinates). A branch-free form (selects
+    // on every flush, the modulo behind one wave-uniform test) measured slower: hash bwd
+    // 0.39-0.41 -> 0.45-0.47 ms (profiles/r06_hash_dense_wrap_ab.log)
     uint32_t gm = cell[0] + static_cast<uint32_t>(b);
 #pragma unroll
     for (int d = 1; d < D; ++d) gm = gm > cell[d] ? gm : cell[d];
@@ -1365,8 +1367,23 @@ extern "C" int anr_hashgrid_bwd_tiles(const anr_hashgrid_desc* d, const float* x
   return ANR_OK;
 }
 
+namespace anr {
+// rows whose bit is clear -> 0 (anr_hashgrid_bwd_rows outside its walker: the dense walker
+// reads every row, and a clear row need not have been written)
+template <typename TG>
+__global__ void zero_clear_rows_kernel(TG* __restrict__ dout, int64_t stride, int64_t M, int ncol,
+                                       const uint32_t* __restrict__ row_nz) {
+  const int64_t n = M * ncol;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < n;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t m = e / ncol;
+    if (((row_nz[m >> 5] >> (m & 31)) & 1u) == 0u) dout[m * stride + e % ncol] = TG(0.0f);
+  }
+}
+}  // namespace anr
+
 extern "C" int anr_hashgrid_bwd_rows(const anr_hashgrid_desc* d, const float* x,
-                                     int64_t x_stride, int64_t M, const void* dout,
+                                     int64_t x_stride, int64_t M, void* dout,
                                      int32_t dout_dtype, int64_t dout_stride, float* dtable,
                                      const uint32_t* row_nz, anr_stream_t stream) {
   using namespace anr;
@@ -1380,11 +1397,26 @@ extern "C" int anr_hashgrid_bwd_rows(const anr_hashgrid_desc* d, const float* x,
   ANR_CHECK_ARG(make_levels(d, &G), "anr_hashgrid_bwd_rows: descriptor not initialised");
   const uint64_t grad_bytes =
       (static_cast<uint64_t>(G.offset[d->n_levels - 1]) + G.size[d->n_levels - 1]) * 2u * 4u;
-  const int64_t K = pick_chunk_v2(M);
+  // chunks of whole 32-row words (the rule's length rounded down, at least one word)
+  int64_t K = pick_chunk_v2(M) / 32 * 32;
+  if (K < 32) K = 32;
+  if (K > 256) K = 256;
   if (!(d->n_dims == 3 && d->n_features == 2 && d->n_levels == 16 && bwd_v2() &&
-        grad_bytes < 0x80000000ull && K % 32 == 0 && K <= 256 && x_stride == 3 &&
-        dout_stride == 32 && M < (int64_t{1} << 31))) {
-    // outside the row-mask walker's shapes: the rows are complete, the mask an optimisation
+        grad_bytes < 0x80000000ull && x_stride == 3 && dout_stride == 32 &&
+        M < (int64_t{1} << 31))) {
+    // outside the row-mask walker's shapes: the clear rows are zeroed in place, then the
+    // dense walker reads every row
+    const int ncol = d->n_levels * d->n_features;
+    const int64_t nb = ceil_div(M * ncol, 256), blocks = nb < 4096 ? nb : 4096;
+    if (dout_dtype == ANR_F16)
+      hipLaunchKernelGGL(zero_clear_rows_kernel<__half>, dim3(static_cast<unsigned>(blocks)),
+                         dim3(256), 0, as_stream(stream), static_cast<__half*>(dout), dout_stride,
+                         M, ncol, row_nz);
+    else
+      hipLaunchKernelGGL(zero_clear_rows_kernel<float>, dim3(static_cast<unsigned>(blocks)),
+                         dim3(256), 0, as_stream(stream), static_cast<float*>(dout), dout_stride,
+                         M, ncol, row_nz);
+    ANR_CHECK_LAUNCH("anr_hashgrid_bwd_rows(zero)");
     return anr_hashgrid_bwd(d, x, x_stride, M, dout, dout_dtype, dout_stride, dtable, stream);
   }
   const dim3 grid(static_cast<unsigned>(ceil_div(ceil_div(M, K), 4))), block(256);

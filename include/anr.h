@@ -192,14 +192,14 @@ int anr_hashgrid_bwd_tiles(const anr_hashgrid_desc* d, const float* x, int64_t x
 
 /* anr_hashgrid_bwd with per-row bits (ABI 5): bit (m % 32) of row_nz[m / 32] set marks a
  * row m of dout with a nonzero value (anr_ingp_field_bwd_ref16_rows writes them); the v2
- * walker loads and walks only those rows. Rows whose bit is clear must be zero in dout
- * (every row is still read when the shape is outside the walker). Same result as
- * anr_hashgrid_bwd; shapes other than 3-D / 2 features / 16 levels / strides (3, 32) /
- * chunks that are a multiple of 32 rows run anr_hashgrid_bwd on the complete rows.
- * Replaces the same call site as anr_hashgrid_bwd (tcnn HashGrid backward,
- * instant_ngp.py:163). */
+ * walker loads and walks only those rows. A row whose bit is clear is taken as zero and
+ * need not have been written (anr_ingp_field_bwd_ref16_rows does not write it). Same
+ * result as anr_hashgrid_bwd on dout with the clear rows zeroed; shapes other than 3-D /
+ * 2 features / 16 levels / strides (3, 32) zero the clear rows IN PLACE (dout is written)
+ * and run anr_hashgrid_bwd. Replaces the same call site as anr_hashgrid_bwd (tcnn HashGrid
+ * backward, instant_ngp.py:163). */
 int anr_hashgrid_bwd_rows(const anr_hashgrid_desc* d, const float* x, int64_t x_stride,
-                          int64_t M, const void* dout, int32_t dout_dtype, int64_t dout_stride,
+                          int64_t M, void* dout, int32_t dout_dtype, int64_t dout_stride,
                           float* dtable, const uint32_t* row_nz, anr_stream_t stream);
 
 /* Level-quad-plane forward (r05; hashgrid.hip forward v9, one lane per sample): the same
@@ -607,7 +607,9 @@ int anr_ingp_field_bwd_ref16_tiles(const anr_mlp_desc* pos, const anr_mlp_desc* 
  * stride d_enc_stride, 8-byte aligned; the reference numerics' dL/denc values are f16
  * numbers, tinycudann/modules.py casts them to the f16 input's dtype, so the rows hold them
  * exactly) and one bit per row in row_nz (ceil(M / 32) words): bit (m % 32) of word m / 32
- * set iff row m has a nonzero value. For anr_hashgrid_bwd_rows (ABI 5).
+ * set iff row m has a nonzero value; every row is written (skipping the clear ones made
+ * partial 128-B line writes: slower, profiles/r06_field_bwd_skip_clear_rows_ab.log). For
+ * anr_hashgrid_bwd_rows (ABI 5).
  * workspace (nullable, 256-byte aligned, anr_ingp_field_bwd_ref16_rows_workspace_bytes(M)
  * bytes): with it the backward runs as a pos pass over the tiles whose dL/dcolor is zero in
  * every row (the dir network adds exactly 0 there) and a full pass over the others, listed

@@ -1468,9 +1468,10 @@ def test_hashgrid_bwd_rows_equals_plain(dev, M):
     """anr_hashgrid_bwd_rows (r06, ABI 5) walks only the rows whose bit is set: with f16
     dL/dy zero on ~70 % of the rows (in runs, as the settled reference numerics leave them)
     and the bits of exactly the nonzero rows, the table gradient equals anr_hashgrid_bwd's
-    up to the f32 atomic order. Clearing the bits of some nonzero rows drops exactly those
-    rows (== the plain walker on dL/dy with them zeroed). M = 300,000 has chunks that are
-    not a multiple of 32 rows: the plain walker runs there on the complete rows."""
+    up to the f32 atomic order, with the clear rows filled with garbage (never read).
+    Clearing the bits of some nonzero rows drops exactly those rows (== the plain walker on
+    dL/dy with them zeroed). M = 300,000: chunks of 64 rows (the rule's 73 rounded down to
+    whole 32-row words)."""
     from atmonr_amd import _lib
 
     cfg = (3, 16, 16, 1.3819, 19)
@@ -1493,19 +1494,53 @@ def test_hashgrid_bwd_rows_equals_plain(dev, M):
         return gt
 
     ga = walk("anr_hashgrid_bwd", dout)
-    gb = walk("anr_hashgrid_bwd_rows", dout, _row_bits(dout))
+    # a clear row is never read: fill the clear rows with garbage for the row walker
+    # (outside the walker's shapes they are zeroed in place first)
+    dg = dout.clone()
+    dg[zero] = 7.0
+    gb = walk("anr_hashgrid_bwd_rows", dg, _row_bits(dout))
     assert torch.isfinite(gb).all()
     assert (ga - gb).abs().max().item() <= 1e-5 * ga.abs().max().item()
     assert ((ga != 0) == (gb != 0)).float().mean().item() > 0.9999
-    if M == 300000:
-        return
     drop = (~zero) & (torch.rand(M, device=dev, generator=g) < 0.2)
     dz = dout.clone()
     dz[drop] = 0.0
-    gc = walk("anr_hashgrid_bwd_rows", dout, _row_bits(dz))
+    gc = walk("anr_hashgrid_bwd_rows", dout.clone(), _row_bits(dz))
     gd = walk("anr_hashgrid_bwd", dz)
     assert (gc - gd).abs().max().item() <= 1e-5 * gd.abs().max().item()
     assert (gc - ga).abs().max().item() > 1e-3 * ga.abs().max().item()
+
+
+def test_hashgrid_bwd_rows_outside_walker_zeroes_clear_rows(dev):
+    """anr_hashgrid_bwd_rows on a shape outside its walker (here: the v1 kernels forced
+    by the test hook) zeroes the clear rows of dL/dy in place, then walks every row: the
+    same gradient as the plain walker on zeroed rows."""
+    from atmonr_amd import _lib
+
+    lib = _lib.load()
+    M = 20000
+    cfg = (3, 16, 16, 1.3819, 19)
+    d = _lib.hashgrid_desc(*cfg[:1], cfg[1], 2, cfg[2], cfg[3], cfg[4])
+    x = _grid_inputs(dev, cfg, M, True).to(dev)
+    g = torch.Generator(device=dev).manual_seed(6)
+    dout = (torch.randn(M, 32, device=dev, generator=g) * 1e-3).half()
+    zero = torch.rand(M, device=dev, generator=g) < 0.6
+    dout[zero] = 0.0
+    dg = dout.clone()
+    dg[zero] = 7.0
+    s = _lib.stream(dev)
+    ga, gb = torch.zeros(d.n_params, device=dev), torch.zeros(d.n_params, device=dev)
+    prev = lib.anr_hashgrid_force_v1(1)
+    try:
+        _lib.call("anr_hashgrid_bwd", ctypes.byref(d), x.data_ptr(), 3, M, dout.data_ptr(),
+                  _lib.F16, 32, ga.data_ptr(), s)
+        _lib.call("anr_hashgrid_bwd_rows", ctypes.byref(d), x.data_ptr(), 3, M, dg.data_ptr(),
+                  _lib.F16, 32, gb.data_ptr(), _row_bits(dout).to(dev).data_ptr(), s)
+        torch.cuda.synchronize()
+    finally:
+        lib.anr_hashgrid_force_v1(prev)
+    assert torch.equal(dg, dout)
+    assert (ga - gb).abs().max().item() <= 1e-5 * ga.abs().max().item()
 
 
 @pytest.mark.parametrize("mma", ["f16", "bf16"])

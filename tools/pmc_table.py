@@ -14,10 +14,13 @@ import os
 import sys
 
 KERNELS = {"hash_fwd": "hashgrid_fwd_planes_kernel<",
-           "hash_bwd": "hashgrid_bwd_v2_kernel<3, float, 3, 32",
+           "hash_bwd": "hashgrid_bwd_v2_kernel<3, __half, 3, 32, false, 6, true>",
+           "hash_bwd_build": "hashgrid_bwd_v2_kernel<3, float, 3, 32",
            "field_fwd": "field::fwd_kernel<64, 2",
            "hash_field_fwd": "hf_fwd_kernel<64, 2",
-           "field_bwd": "field::bwd_rt_kernel<64, 2, true, false",
+           "field_bwd": "field::bwd_rt_kernel<64, 2, true, false, false, 4>",
+           "field_bwd_list": "field::bwd_rt_kernel<64, 2, true, false, false, 3>",
+           "field_bwd_build": "field::bwd_rt_kernel<64, 2, true, false, false, 0>",
            "sampler": "sample_uniform_bins_kernel",
            "comp_fwd": "ref16::fwd_kernel<",
            "comp_bwd": "ref16::bwd_kernel<",

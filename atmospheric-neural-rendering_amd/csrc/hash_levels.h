@@ -10,6 +10,10 @@
 // gather at the run leaders only (see there); 0 = every lane gathers, 64 = every level
 #define HASH_DEDUP 64
 #endif
+#ifndef HASH_FMA_MIX
+// Raw2<__half>::fma2 as v_fma_mix_f32 (1) or f16 -> f32 conversions + f32 FMAs (0)
+#define HASH_FMA_MIX 1
+#endif
 
 namespace anr {
 
@@ -101,10 +105,19 @@ struct Raw2<__half> {
   __device__ static type from_lane(type v, int src) {
     return static_cast<type>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
   }
+  // a0 += wt * f32(lo), a1 += wt * f32(hi): the f16 -> f32 conversion is exact, so one
+  // mixed-precision FMA per feature is the same single-rounded result as the conversion
+  // plus an f32 FMA (hipcc emits the two: it forms v_fma_mix only when f32 denormals are
+  // flushed; these products are far above the f32 denormal range)
   __device__ static void fma2(float wt, type v, float& a0, float& a1) {
+#if HASH_FMA_MIX
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[0,1,0]" : "+v"(a0) : "v"(wt), "v"(v));
+    asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "+v"(a1) : "v"(wt), "v"(v));
+#else
     const __half2 h = __builtin_bit_cast(__half2, v);
     a0 = fmaf(wt, __low2float(h), a0);
     a1 = fmaf(wt, __high2float(h), a1);
+#endif
   }
 };
 template <>

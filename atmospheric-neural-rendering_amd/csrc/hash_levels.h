@@ -101,6 +101,10 @@ struct Raw2<__half> {
   __device__ static type load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
   }
+  // voff per lane, soff wave-uniform (the level's base: the instruction's SGPR offset)
+  __device__ static type load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+  }
   // the value of lane src (ds_bpermute)
   __device__ static type from_lane(type v, int src) {
     return static_cast<type>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
@@ -126,6 +130,9 @@ struct Raw2<float> {
   static constexpr uint32_t bytes = 8;
   __device__ static type load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  }
+  __device__ static type load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
   }
   __device__ static type from_lane(type v, int src) {
     type o;
@@ -177,30 +184,52 @@ __device__ __forceinline__ void plane_quad(const GridLevels& G, int n_levels, in
       g[d] = static_cast<uint32_t>(static_cast<int>(fl));
       w[d] = p - fl;
     }
-    uint32_t comp[D][2];
-    li.dims(g, comp);
-    uint32_t idx[1 << D], sum[1 << D];
-#pragma unroll
-    for (int c = 0; c < (1 << D); ++c) {
-      uint32_t hx = 0u, sm = 0u;
+    // idx: the corners' byte offsets within the level (its base goes to the loads' SGPR
+    // offset). Hashed levels (wave-uniform branch) hash byte-scaled components: R::bytes is
+    // a power of two, so (a*k ^ b*k ^ c*k) & (T-1)*k == ((a ^ b ^ c) & (T-1)) * k, bits
+    // lost past 2^32 included (they are above the mask); dense levels scale after the wrap
+    uint32_t idx[1 << D];
+    if (li.hashed) {
+      uint32_t comp[D][2];
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        hx ^= comp[d][(c >> d) & 1];
-        sm += comp[d][(c >> d) & 1];
+        const uint32_t m = li.mul[d] * R::bytes;
+        comp[d][0] = g[d] * m;
+        comp[d][1] = comp[d][0] + m;
       }
-      sum[c] = sm;
-      idx[c] = li.hashed ? (hx & hmask) : sm;
-    }
-    uint32_t gmax = g[0];
+      const uint32_t hmb = hmask * R::bytes;
 #pragma unroll
-    for (int d = 1; d < D; ++d) gmax = gmax > g[d] ? gmax : g[d];
-    if (!li.hashed && gmax >= res - 1u) {
+      for (int c = 0; c < (1 << D); ++c) {
+        uint32_t hx = 0u;
 #pragma unroll
-      for (int c = 0; c < (1 << D); ++c)
-        if (sum[c] >= T) {
-          const uint32_t s1 = sum[c] - T;
-          idx[c] = s1 < T ? s1 : sum[c] % T;
-        }
+        for (int d = 0; d < D; ++d) hx ^= comp[d][(c >> d) & 1];
+        idx[c] = hx & hmb;
+      }
+    } else {
+      uint32_t comp[D][2];
+      li.dims(g, comp);
+      uint32_t sum[1 << D];
+#pragma unroll
+      for (int c = 0; c < (1 << D); ++c) {
+        uint32_t sm = 0u;
+#pragma unroll
+        for (int d = 0; d < D; ++d) sm += comp[d][(c >> d) & 1];
+        sum[c] = sm;
+        idx[c] = sm;
+      }
+      uint32_t gmax = g[0];
+#pragma unroll
+      for (int d = 1; d < D; ++d) gmax = gmax > g[d] ? gmax : g[d];
+      if (gmax >= res - 1u) {
+#pragma unroll
+        for (int c = 0; c < (1 << D); ++c)
+          if (sum[c] >= T) {
+            const uint32_t s1 = sum[c] - T;
+            idx[c] = s1 < T ? s1 : sum[c] % T;
+          }
+      }
+#pragma unroll
+      for (int c = 0; c < (1 << D); ++c) idx[c] *= R::bytes;
     }
     typename R::type val[1 << D];
     bool plain = true;
@@ -229,7 +258,7 @@ __device__ __forceinline__ void plane_quad(const GridLevels& G, int n_levels, in
         const int src = 63 - static_cast<int>(__clzll(static_cast<long long>(below)));
         if (lead) {
 #pragma unroll
-          for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, base + idx[c] * R::bytes);
+          for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, idx[c], base);
         }
 #pragma unroll
         for (int c = 0; c < (1 << D); ++c) val[c] = R::from_lane(val[c], src);
@@ -237,7 +266,7 @@ __device__ __forceinline__ void plane_quad(const GridLevels& G, int n_levels, in
     }
     if (plain) {
 #pragma unroll
-      for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, base + idx[c] * R::bytes);
+      for (int c = 0; c < (1 << D); ++c) val[c] = R::load(rt, idx[c], base);
     }
     float a0 = 0.0f, a1 = 0.0f;
 #pragma unroll

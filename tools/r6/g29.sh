@@ -1,0 +1,13 @@
+#!/bin/bash
+# r6: row-walker chunk length: ANR_HASH_KB=128 against the rule's 256, at 8,192 and 1,024 rays
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r6_g29; mkdir -p $O
+for rep in 1 2; do
+  for k in 256 128; do
+    ANR_HASH_KB=$k timeout -k 10 300 python -u bench.py --no-alt-numerics --no-cpu-baseline > $O/bench_k${k}_$rep.json.log 2>&1 || { tail -30 $O/bench_k${k}_$rep.json.log; exit 1; }
+    python3 tools/r5/bench_line.py $O/bench_k${k}_$rep.json.log "K=$k $rep"
+    ANR_HASH_KB=$k timeout -k 10 300 python -u bench.py --batch 1024 --no-alt-numerics --no-cpu-baseline > $O/b1024_k${k}_$rep.json.log 2>&1 || { tail -30 $O/b1024_k${k}_$rep.json.log; exit 1; }
+    python3 tools/r5/bench_line.py $O/b1024_k${k}_$rep.json.log "b1024 K=$k $rep"
+  done
+done

@@ -34,6 +34,12 @@ def test_abi_version_and_struct_sizes():
     from atmonr_amd import _lib
 
     assert _lib.load().anr_abi_version() == 5
+    # __graft_entry__.build() checks the built library against the header's define
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                       "anr.h")
+    with open(hdr) as f:
+        want = next(int(ln.split()[2]) for ln in f if ln.startswith("#define ANR_ABI_VERSION"))
+    assert want == _lib.load().anr_abi_version()
     assert ctypes.sizeof(_lib.PrepParams) == 96
     assert ctypes.sizeof(_lib.MlpDesc) == 32
 

@@ -3,4 +3,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=r06_final bash tools/r6/prof_final.sh
-bash tools/r6/g29.sh
+bash tools/archive/r6/g29.sh

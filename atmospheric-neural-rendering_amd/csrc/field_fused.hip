@@ -1066,6 +1066,14 @@ __global__ void __launch_bounds__(256) bwd_rt_kernel(Args a, float target, int64
   constexpr int MT = 2, TR = 16 * MT, NP = MT / 2;
   using N = Net<W, NHD>;
   constexpr int NT = N::NT, KB = N::KB;
+  if constexpr (REF == 3) {
+    // the list pass: a block none of whose waves has a listed tile leaves before its
+    // prologue (weights into LDS, sums zeroed): in the settled state the list is empty and
+    // the whole launch was ~26 us of prologues (rocprof r06_c). Block-uniform exit.
+    const uint32_t cnt = static_cast<uint32_t>(
+        __builtin_amdgcn_readfirstlane(static_cast<int>(*a.tile_count)));
+    if (static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) >= cnt) return;
+  }
   __shared__ __attribute__((aligned(16))) _Float16 wsm[N::n_packed];
   // the block's dW partials (pos parameters, then dir), summed here before the one global
   // flush per block
